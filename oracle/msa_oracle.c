@@ -1,0 +1,525 @@
+/*
+ * msa_oracle.c -- CPU restatement of the reference's hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (the HIP library, the C++
+ * drop-in layer, the Python package) links, loads or calls this file.  Only
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use it, and
+ * only as the checker / the timed CPU baseline.
+ *
+ * Parity pinning: every function below was checked against golden vectors
+ * produced by the reference's own sources compiled unmodified from
+ * /root/reference (oracle/Makefile -> oracle/_ref/libref.so, generator
+ * tests/golden/make_golden.py).  See DESIGN.md "Oracle".
+ *
+ * Functions and the reference code each one restates:
+ *   orc_subproblem_tables  subproblem_alignment.h:36-74 (ctor, A/B swap),
+ *                          subproblem_alignment.cpp:357-399 (non_parallel_tables,
+ *                          bit-identical to compute_tables :329-332, borders
+ *                          :212-227, :259-292)
+ *   orc_subproblem_traceback subproblem_alignment.cpp:105-172 (find_alignment,
+ *                          tie order, quirks Q1 (:147,:170) and Q2 (:151))
+ *   orc_print_seq          main_alignment.cpp:32-55
+ *   orc_main_alignment     main_alignment.cpp:11-22 (OptimalAlignmentMapThread),
+ *                          :202-351 (single-subproblem path), :353-410
+ *   orc_partial_tables / orc_partial_partition
+ *                          partial.cpp:9-163 with two's-complement wrap (the
+ *                          reference's -O0 behaviour)
+ *   orc_sw                 build extension (Smith-Waterman local, affine/linear),
+ *                          "reference-anchored": same cell recurrence family
+ *   orc_banded_ref         build extension: reference Gotoh (T1/T2/T3) restricted
+ *                          to |i-j| <= w; equals orc_subproblem_tables when w >= max(m,n)
+ *   orc_checksum_h         order-independent 64-bit digest of an int32 matrix
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ORC_OK 0
+#define ORC_ERR_ARG -1
+#define ORC_ERR_CAP -2
+#define ORC_ERR_NOMATCH -3 /* reference would read an uninitialised node (non-integral g/h) */
+#define ORC_ERR_NOMEM -4
+
+typedef struct {
+  uint64_t i;
+  uint64_t j;
+  int32_t t;
+  int32_t pad;
+} orc_node;
+
+static inline double dmax(double a, double b) { return a > b ? a : b; }
+/* std::max(a,b) returns a when !(a < b): for the values here (no NaN) the
+ * value is the same as dmax, which is all that matters. */
+
+/* ---------------------------------------------------------------------------
+ * Reference Subproblem: tables.
+ *   A, B: the caller's 1-based arrays (A[0] never read).
+ *   After the constructor's swap (m > n -> swap), tables are (m'+1) x (n'+1),
+ *   row-major, row stride n'+1.  *invert reports whether the swap happened.
+ * ------------------------------------------------------------------------- */
+int orc_subproblem_tables(const char* A_in, const char* B_in, uint64_t m_in, uint64_t n_in,
+                          uint64_t idA_in, uint64_t idB_in, int start_type, double g, double h,
+                          double* T1, double* T2, double* T3, int* invert) {
+  const char *A, *B;
+  uint64_t m, n, idA, idB;
+  if (m_in <= n_in) {
+    A = A_in; B = B_in; m = m_in; n = n_in; idA = idA_in; idB = idB_in; *invert = 0;
+  } else {
+    A = B_in; B = A_in; m = n_in; n = m_in; idA = idB_in; idB = idA_in; *invert = 1;
+  }
+  const uint64_t W = n + 1;
+  const double NI = -INFINITY;
+#define T(tab, i, j) tab[(uint64_t)(i) * W + (j)]
+  /* row 0: compute_row(0), subproblem_alignment.cpp:259-280 */
+  T(T1, 0, 0) = NI; T(T2, 0, 0) = NI; T(T3, 0, 0) = NI;
+  if (start_type == 1 || start_type == -1) T(T1, 0, 0) = 0;
+  else if (start_type == -2) T(T2, 0, 0) = 0;
+  else if (start_type == -3) T(T3, 0, 0) = 0;
+  for (uint64_t j = 1; j <= n; j++) { /* ComputeFirstRowMapThread :212-227 */
+    T(T1, 0, j) = NI;
+    T(T3, 0, j) = NI;
+    if (start_type == -2) T(T2, 0, j) = -g * (double)j;
+    else if (start_type == 1 || start_type == 3) T(T2, 0, j) = NI;
+    else T(T2, 0, j) = -h - g * (double)j;
+  }
+  for (uint64_t i = 1; i <= m; i++) {
+    T(T1, i, 0) = NI; T(T2, i, 0) = NI; /* :282-292 */
+    if (start_type == -3) T(T3, i, 0) = -g * (double)i;
+    else if (start_type == 1 || start_type == 2) T(T3, i, 0) = NI;
+    else T(T3, i, 0) = -h - g * (double)i;
+    const char a = A[idA + i];
+    for (uint64_t j = 1; j <= n; j++) { /* :396-398 */
+      const double f = (a == B[idB + j]) ? 1.0 : 0.0;
+      T(T1, i, j) = f + dmax(dmax(T(T1, i - 1, j - 1), T(T2, i - 1, j - 1)), T(T3, i - 1, j - 1));
+      T(T3, i, j) = dmax(dmax(T(T1, i - 1, j) - g - h, T(T2, i - 1, j) - g - h), T(T3, i - 1, j) - g);
+      T(T2, i, j) = dmax(dmax(T(T1, i, j - 1) - g - h, T(T2, i, j - 1) - g), T(T3, i, j - 1) - g - h);
+    }
+  }
+  return ORC_OK;
+}
+
+/* ---------------------------------------------------------------------------
+ * Reference Subproblem::find_alignment (subproblem_alignment.cpp:105-172).
+ *   Works on the (already swapped) problem: A,B,m,n,idA,idB are the values the
+ *   Subproblem object holds after its constructor.
+ *   nodes[0..*n_nodes) = the list from alignment_begin to alignment_end.
+ *   end_node receives alignment_end (always written).
+ * ------------------------------------------------------------------------- */
+int orc_subproblem_traceback(const char* A, const char* B, uint64_t m, uint64_t n, uint64_t idA,
+                             uint64_t idB, int end_type, double g, double h, const double* T1,
+                             const double* T2, const double* T3, orc_node* nodes, uint64_t cap,
+                             uint64_t* n_nodes, orc_node* end_node) {
+  const uint64_t W = n + 1;
+  uint64_t i = m, j = n;
+  orc_node cur;
+  /* h_prime, subproblem_alignment.h:91-96 */
+#define HPRIME(k) (((k) == end_type && end_type <= -2) ? h : 0.0)
+  if (end_type > 0) {
+    cur.t = end_type;
+    if (end_type == 1) { cur.i = i + idA; cur.j = j + idB; }
+    else if (end_type == 2) { cur.i = 0; cur.j = j + idB; }
+    else { cur.i = i + idA; cur.j = 0; }
+  } else {
+    const double t1 = T(T1, m, n);
+    const double t2 = T(T2, m, n) + HPRIME(-2);
+    const double t3 = T(T3, m, n) + HPRIME(-3);
+    if (t1 >= t2 && t1 >= t3) { cur.t = 1; cur.i = i + idA; cur.j = j + idB; }
+    else if (t2 >= t1 && t2 >= t3) { cur.t = 2; cur.i = 0; cur.j = j + idB; }
+    else { cur.t = 3; cur.i = i + idA; cur.j = 0; }
+  }
+  cur.pad = 0;
+  *end_node = cur;
+  /* The reference prepends nodes while walking back; we collect them in
+   * reverse and flip at the end.  The final list skips the last-created node
+   * (Q1: alignment_begin = curr_point->next). */
+  uint64_t cnt = 0; /* number of created nodes, including the end node */
+  /* worst case path length m+n+1 */
+  orc_node* tmp = (orc_node*)malloc(sizeof(orc_node) * (m + n + 2));
+  if (!tmp) return ORC_ERR_NOMEM;
+  tmp[cnt++] = cur;
+  int ct = cur.t;
+  while (i > 0 && j > 0) {
+    orc_node nw;
+    nw.pad = 0;
+    const char a = A[idA + i];
+    const double f = (a == B[idB + j]) ? 1.0 : 0.0;
+    if (ct == 1) {
+      const double v = T(T1, i, j);
+      if (v == f + T(T1, i - 1, j - 1)) { nw.t = 1; nw.i = i - 1 + idA; nw.j = j - 1 + idA; } /* Q2 */
+      else if (v == f + T(T2, i - 1, j - 1)) { nw.t = 2; nw.i = 0; nw.j = j - 1 + idB; }
+      else if (v == f + T(T3, i - 1, j - 1)) { nw.t = 3; nw.i = i - 1 + idA; nw.j = 0; }
+      else { free(tmp); return ORC_ERR_NOMATCH; }
+      i--; j--;
+    } else if (ct == 2) {
+      const double v = T(T2, i, j);
+      if (v == -g - h + T(T1, i, j - 1)) { nw.t = 1; nw.i = i + idA; nw.j = j - 1 + idB; }
+      else if (v == -g + T(T2, i, j - 1)) { nw.t = 2; nw.i = 0; nw.j = j - 1 + idB; }
+      else if (v == -g - h + T(T3, i, j - 1)) { nw.t = 3; nw.i = i + idA; nw.j = 0; }
+      else { free(tmp); return ORC_ERR_NOMATCH; }
+      j--;
+    } else {
+      const double v = T(T3, i, j);
+      if (v == -g - h + T(T1, i - 1, j)) { nw.t = 1; nw.i = i - 1 + idA; nw.j = j + idB; }
+      else if (v == -g - h + T(T2, i - 1, j)) { nw.t = 2; nw.i = 0; nw.j = j + idB; }
+      else if (v == -g + T(T3, i - 1, j)) { nw.t = 3; nw.i = i - 1 + idA; nw.j = 0; }
+      else { free(tmp); return ORC_ERR_NOMATCH; }
+      i--;
+    }
+    ct = nw.t;
+    tmp[cnt++] = nw;
+  }
+#undef HPRIME
+  /* list = tmp[cnt-2], tmp[cnt-3], ..., tmp[0]  (tmp[cnt-1] dropped) */
+  const uint64_t len = cnt - 1;
+  *n_nodes = len;
+  if (len > cap) { free(tmp); return ORC_ERR_CAP; }
+  for (uint64_t k = 0; k < len; k++) nodes[k] = tmp[cnt - 2 - k];
+  free(tmp);
+  return ORC_OK;
+}
+#undef T
+
+/* main_alignment.cpp:32-55.  out1/out2 receive len chars + NUL.  Indices past
+ * the caller's buffers (only possible in the reference's m>n quirk Q3) print '?'
+ * here; the reference reads out of bounds there. */
+void orc_print_seq(const char* A, const char* B, uint64_t lenA, uint64_t lenB, const orc_node* nodes,
+                   uint64_t len, char* out1, char* out2) {
+  for (uint64_t k = 0; k < len; k++) {
+    const orc_node* p = &nodes[k];
+    out1[k] = (p->t == 1 || p->t == 3) ? (p->i <= lenA ? A[p->i] : '?') : '-';
+    out2[k] = (p->t == 1 || p->t == 2) ? (p->j <= lenB ? B[p->j] : '?') : '-';
+  }
+  out1[len] = 0;
+  out2[len] = 0;
+}
+
+/* The observable output of main_alignment_function(A,B,m,n,p,g,h) for the live
+ * single-subproblem partition [(0,0,-1),(m,n,1)]: "bp1".."bp4" from
+ * OptimalAlignmentMapThread, then print_seq's two lines.  p only changes the
+ * reference's thread count (bit-identical results), so it is not an input.
+ * Writes the text (NUL-terminated) into out; returns bytes written or <0. */
+int64_t orc_main_alignment(const char* A, const char* B, uint64_t m, uint64_t n, double g, double h,
+                           char* out, uint64_t cap, double* score) {
+  int inv;
+  const uint64_t mm = m <= n ? m : n, nn = m <= n ? n : m;
+  double* T1 = (double*)malloc(sizeof(double) * (mm + 1) * (nn + 1));
+  double* T2 = (double*)malloc(sizeof(double) * (mm + 1) * (nn + 1));
+  double* T3 = (double*)malloc(sizeof(double) * (mm + 1) * (nn + 1));
+  orc_node* nodes = (orc_node*)malloc(sizeof(orc_node) * (m + n + 2));
+  if (!T1 || !T2 || !T3 || !nodes) return ORC_ERR_NOMEM;
+  orc_subproblem_tables(A, B, m, n, 0, 0, -1, g, h, T1, T2, T3, &inv);
+  const char* sA = inv ? B : A;
+  const char* sB = inv ? A : B;
+  uint64_t len = 0;
+  orc_node endn;
+  /* end_type = -partial_bp[1].t = -1 (main_alignment.cpp:251) */
+  int rc = orc_subproblem_traceback(sA, sB, mm, nn, 0, 0, -1, g, h, T1, T2, T3, nodes, m + n + 2,
+                                    &len, &endn);
+  if (score) {
+    const uint64_t W = nn + 1;
+    double t1 = T1[mm * W + nn], t2 = T2[mm * W + nn], t3 = T3[mm * W + nn];
+    *score = dmax(dmax(t1, t2), t3);
+  }
+  free(T1); free(T2); free(T3);
+  if (rc != ORC_OK) { free(nodes); return rc; }
+  const char* hdr = "bp1\nbp1.2\nbp2\nbp3\nbp4\n";
+  const uint64_t need = strlen(hdr) + 2 * (len + 1) + 1;
+  if (need > cap) { free(nodes); return ORC_ERR_CAP; }
+  char* l1 = (char*)malloc(len + 1);
+  char* l2 = (char*)malloc(len + 1);
+  orc_print_seq(A, B, m, n, nodes, len, l1, l2); /* unswapped arrays, as the reference (Q3) */
+  uint64_t o = 0;
+  memcpy(out + o, hdr, strlen(hdr)); o += strlen(hdr);
+  memcpy(out + o, l1, len); o += len; out[o++] = '\n';
+  memcpy(out + o, l2, len); o += len; out[o++] = '\n';
+  out[o] = 0;
+  free(l1); free(l2); free(nodes);
+  return (int64_t)o;
+}
+
+/* ---------------------------------------------------------------------------
+ * partial.cpp restated with two's-complement wrap (int32 arithmetic done in
+ * uint32 so the C here has no UB).  Table shapes as the reference:
+ *   T*  : (m+1) x (n+1), row stride n+1
+ *   TR* : (m+2) x (n+2), row stride n+2
+ * A,B are indexed A[i-1], B[j-1] (partial.cpp:105,119).
+ * ------------------------------------------------------------------------- */
+static inline int32_t wadd(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
+static inline int32_t wsub(int32_t a, int32_t b) { return (int32_t)((uint32_t)a - (uint32_t)b); }
+static inline int32_t imax3(int32_t a, int32_t b, int32_t c) {
+  int32_t x = a > b ? a : b;
+  return x > c ? x : c;
+}
+
+int orc_partial_tables(const char* A, const char* B, uint64_t m, uint64_t n, double g, double h,
+                       int start_type, int end_type, int32_t* T1, int32_t* T2, int32_t* T3,
+                       int32_t* R1, int32_t* R2, int32_t* R3) {
+  const int32_t GH = (int32_t)(g + h), G = (int32_t)g;
+  const uint64_t W = n + 1, WR = n + 2;
+  /* initializeTables :13-31 */
+  for (uint64_t k = 0; k < (m + 1) * W; k++) T1[k] = T2[k] = T3[k] = INT32_MIN;
+  if (start_type == 1) T1[0] = 0;
+  else if (start_type == 2) for (uint64_t j = 1; j <= n; j++) T2[j] = (int32_t)((uint32_t)(-GH) * (uint32_t)j);
+  else if (start_type == 3) for (uint64_t i = 1; i <= m; i++) T3[i * W] = (int32_t)((uint32_t)(-GH) * (uint32_t)i);
+  /* initializeReverseTables :33-51 */
+  for (uint64_t k = 0; k < (m + 2) * WR; k++) R1[k] = R2[k] = R3[k] = INT32_MIN;
+  if (end_type == 1) R1[(m + 1) * WR + n + 1] = 0;
+  else if (end_type == 2) for (uint64_t j = n; j > 0; j--) R2[(m + 1) * WR + j] = (int32_t)((uint32_t)(-GH) * (uint32_t)(n - j + 1));
+  else if (end_type == 3) for (uint64_t i = m; i > 0; i--) R3[i * WR + n + 1] = (int32_t)((uint32_t)(-GH) * (uint32_t)(m - i + 1));
+  /* fillTablesParallel :53-65 */
+  for (uint64_t i = 1; i <= m; i++)
+    for (uint64_t j = 1; j <= n; j++) {
+      const int32_t s = (A[i - 1] == B[j - 1]) ? 0 : 1;
+      T1[i * W + j] = imax3(wadd(T1[(i - 1) * W + j - 1], s), wadd(T2[(i - 1) * W + j - 1], s),
+                            wadd(T3[(i - 1) * W + j - 1], s));
+      T2[i * W + j] = imax3(wsub(T1[i * W + j - 1], GH), wsub(T2[i * W + j - 1], G), wsub(T3[i * W + j - 1], GH));
+      T3[i * W + j] = imax3(wsub(T1[(i - 1) * W + j], GH), wsub(T2[(i - 1) * W + j], GH), wsub(T3[(i - 1) * W + j], G));
+    }
+  /* fillReverseTablesParallel :67-79 */
+  for (uint64_t i = m; i >= 1; i--)
+    for (uint64_t j = n; j >= 1; j--) {
+      const int32_t s = (A[i - 1] == B[j - 1]) ? 0 : 1;
+      R1[i * WR + j] = imax3(wadd(R1[(i + 1) * WR + j + 1], s), wadd(R2[(i + 1) * WR + j + 1], s),
+                             wadd(R3[(i + 1) * WR + j + 1], s));
+      R2[i * WR + j] = imax3(wsub(R1[i * WR + j + 1], GH), wsub(R2[i * WR + j + 1], G), wsub(R3[i * WR + j + 1], GH));
+      R3[i * WR + j] = imax3(wsub(R1[(i + 1) * WR + j], GH), wsub(R2[(i + 1) * WR + j], GH), wsub(R3[(i + 1) * WR + j], G));
+    }
+  return ORC_OK;
+}
+
+/* findPartitionParallel (partial.cpp:81-146); out receives p+1 nodes
+ * (sorted by (i,j) with a stable sort; the reference's std::sort is an
+ * insertion sort -- hence stable -- for the <=16 elements of every p<=15). */
+int orc_partial_partition(const int32_t* T1, const int32_t* T2, const int32_t* T3, const int32_t* R1,
+                          const int32_t* R2, const int32_t* R3, uint64_t m, uint64_t n, uint64_t p,
+                          double h, orc_node* out, uint64_t cap, uint64_t* n_out) {
+  if (p == 0) return ORC_ERR_ARG;
+  const uint64_t W = n + 1, WR = n + 2;
+  const int32_t H = (int32_t)h;
+  const uint64_t bm = m / p, bn = n / p;
+  uint64_t cnt = 0;
+  if (cap < p + 1) return ORC_ERR_CAP;
+  out[cnt].i = 0; out[cnt].j = 0; out[cnt].t = -1; out[cnt].pad = 0; cnt++;
+#define VAL(i, j) imax3(wadd(T1[(i) * W + (j)], R1[(i) * WR + (j)]), \
+                        wadd(wadd(T2[(i) * W + (j)], R2[(i) * WR + (j)]), H), \
+                        wadd(wadd(T3[(i) * W + (j)], R3[(i) * WR + (j)]), H))
+#define TYPE(i, j) ((T1[(i) * W + (j)] >= T2[(i) * W + (j)] && T1[(i) * W + (j)] >= T3[(i) * W + (j)]) ? 1 \
+                    : (T2[(i) * W + (j)] >= T3[(i) * W + (j)]) ? 2 : 3)
+  for (uint64_t k = 1; k < p; k++) {
+    int32_t mr = INT32_MIN, mc = INT32_MIN;
+    orc_node br = {0, 0, 0, 0}, bc = {0, 0, 0, 0};
+    for (uint64_t i = k * bm; i < (k + 1) * bm && i <= m; i++)
+      for (uint64_t j = 1; j <= n; j++) {
+        const int32_t v = VAL(i, j);
+        if (v > mr) { mr = v; br.i = i; br.j = j; br.t = TYPE(i, j); }
+      }
+    for (uint64_t j = k * bn; j < (k + 1) * bn && j <= n; j++)
+      for (uint64_t i = 1; i <= m; i++) {
+        const int32_t v = VAL(i, j);
+        if (v > mc) { mc = v; bc.i = i; bc.j = j; bc.t = TYPE(i, j); }
+      }
+    out[cnt++] = (mr > mc) ? br : bc;
+  }
+#undef VAL
+#undef TYPE
+  out[cnt].i = m; out[cnt].j = n; out[cnt].t = 1; out[cnt].pad = 0; cnt++;
+  /* stable insertion sort by (i, j) */
+  for (uint64_t a = 1; a < cnt; a++) {
+    orc_node key = out[a];
+    uint64_t b = a;
+    while (b > 0 && ((key.i < out[b - 1].i) || (key.i == out[b - 1].i && key.j < out[b - 1].j))) {
+      out[b] = out[b - 1];
+      b--;
+    }
+    out[b] = key;
+  }
+  *n_out = cnt;
+  return ORC_OK;
+}
+
+/* ---------------------------------------------------------------------------
+ * Smith-Waterman local alignment (build extension; no reference equivalent).
+ *   s(a,b) = a==b ? match : mismatch;  gap of length L costs open + (L-1)*extend
+ *   (linear gap g  <=>  open == extend == g).
+ *   E(i,j) = max(E(i,j-1) - ext, H(i,j-1) - open)    horizontal (consumes B)
+ *   F(i,j) = max(F(i-1,j) - ext, H(i-1,j) - open)    vertical   (consumes A)
+ *   H(i,j) = max(0, H(i-1,j-1) + s, E, F);  H(0,*) = H(*,0) = 0, E(*,0)=F(0,*)=-inf
+ *   score = max H; end = first maximum in row-major order (min i, then min j).
+ *   A, B are 0-based here (A[i-1] is row i).
+ *   Traceback (documented tie order): in H: stop if H==0, else diag if
+ *   H==Hd+s, else E if H==E, else F.  In E: open if E==H(i,j-1)-open else
+ *   extend.  In F: open if F==H(i-1,j)-open else extend.
+ *   cigar (optional): run-length string of M/D/I from start to end, D =
+ *   horizontal move (consumes B), I = vertical move (consumes A).
+ *   Hout (optional) receives H, (m+1) x (n+1) row-major.
+ * ------------------------------------------------------------------------- */
+int orc_sw(const char* A, const char* B, uint64_t m, uint64_t n, int32_t match, int32_t mismatch,
+           int32_t open, int32_t ext, int32_t* Hout, int32_t* score, uint64_t* end_i, uint64_t* end_j,
+           uint64_t* beg_i, uint64_t* beg_j, char* cigar, uint64_t cigar_cap) {
+  const uint64_t W = n + 1;
+  const int32_t NEG = INT32_MIN / 4;
+  int32_t* H = Hout;
+  int own = 0;
+  const int want_tb = (cigar != NULL) || (beg_i != NULL);
+  int32_t *E = NULL, *F = NULL;
+  if (!H) { H = (int32_t*)malloc(sizeof(int32_t) * (m + 1) * W); own = 1; }
+  if (want_tb) {
+    E = (int32_t*)malloc(sizeof(int32_t) * (m + 1) * W);
+    F = (int32_t*)malloc(sizeof(int32_t) * (m + 1) * W);
+  }
+  if (!H || (want_tb && (!E || !F))) return ORC_ERR_NOMEM;
+  int32_t* Frow = (int32_t*)malloc(sizeof(int32_t) * W);
+  for (uint64_t j = 0; j <= n; j++) { H[j] = 0; Frow[j] = NEG; if (want_tb) { E[j] = NEG; F[j] = NEG; } }
+  int32_t best = 0;
+  uint64_t bi = 0, bj = 0;
+  for (uint64_t i = 1; i <= m; i++) {
+    int32_t e = NEG;
+    H[i * W] = 0;
+    if (want_tb) { E[i * W] = NEG; F[i * W] = NEG; }
+    const char a = A[i - 1];
+    for (uint64_t j = 1; j <= n; j++) {
+      const int32_t s = (a == B[j - 1]) ? match : mismatch;
+      const int32_t el = e - ext, eo = H[i * W + j - 1] - open;
+      e = el > eo ? el : eo;
+      const int32_t fu = Frow[j] - ext, fo = H[(i - 1) * W + j] - open;
+      const int32_t f = fu > fo ? fu : fo;
+      Frow[j] = f;
+      int32_t v = H[(i - 1) * W + j - 1] + s;
+      if (e > v) v = e;
+      if (f > v) v = f;
+      if (v < 0) v = 0;
+      H[i * W + j] = v;
+      if (want_tb) { E[i * W + j] = e; F[i * W + j] = f; }
+      if (v > best) { best = v; bi = i; bj = j; }
+    }
+  }
+  *score = best;
+  if (end_i) *end_i = bi;
+  if (end_j) *end_j = bj;
+  int rc = ORC_OK;
+  if (want_tb) {
+    /* walk back; ops collected reversed */
+    char* ops = (char*)malloc(m + n + 2);
+    uint64_t nops = 0, i = bi, j = bj;
+    int st = 0; /* 0=H,1=E,2=F */
+    if (best > 0) {
+      while (1) {
+        if (st == 0) {
+          const int32_t v = H[i * W + j];
+          if (v == 0) break;
+          const int32_t s = (A[i - 1] == B[j - 1]) ? match : mismatch;
+          if (v == H[(i - 1) * W + j - 1] + s) { ops[nops++] = 'M'; i--; j--; if (i == 0 || j == 0) break; }
+          else if (v == E[i * W + j]) st = 1;
+          else st = 2;
+        } else if (st == 1) {
+          const int32_t v = E[i * W + j];
+          ops[nops++] = 'D';
+          st = (v == H[i * W + j - 1] - open) ? 0 : 1;
+          j--;
+        } else {
+          const int32_t v = F[i * W + j];
+          ops[nops++] = 'I';
+          st = (v == H[(i - 1) * W + j] - open) ? 0 : 2;
+          i--;
+        }
+      }
+    }
+    if (beg_i) *beg_i = i + 1;
+    if (beg_j) *beg_j = j + 1;
+    if (cigar) {
+      uint64_t o = 0;
+      int64_t k = (int64_t)nops - 1;
+      while (k >= 0) {
+        char c = ops[k];
+        uint64_t run = 0;
+        while (k >= 0 && ops[k] == c) { run++; k--; }
+        char buf[32];
+        int l = 0;
+        uint64_t r = run;
+        char tmp[24];
+        int tl = 0;
+        do { tmp[tl++] = (char)('0' + r % 10); r /= 10; } while (r);
+        while (tl) buf[l++] = tmp[--tl];
+        buf[l++] = c;
+        if (o + (uint64_t)l + 1 > cigar_cap) { rc = ORC_ERR_CAP; break; }
+        memcpy(cigar + o, buf, (size_t)l);
+        o += (uint64_t)l;
+      }
+      if (rc == ORC_OK) cigar[o] = 0;
+    }
+    free(ops);
+    free(E); free(F);
+  }
+  free(Frow);
+  if (own) free(H);
+  return rc;
+}
+
+/* ---------------------------------------------------------------------------
+ * Banded reference Gotoh (build extension for config C3): the recurrence and
+ * borders of orc_subproblem_tables with start_type -1, every cell with
+ * |i - j| > w treated as -inf (never computed).  Requires |m-n| <= w.
+ * score = max(T1,T2,T3)[m][n].  Hout (optional, (m+1)x(n+1) row-major) gets
+ * max(T1,T2,T3) as int32 for in-band interior cells and 0 elsewhere.
+ * Uses O(n) memory per table row pair.
+ * ------------------------------------------------------------------------- */
+int orc_banded_ref(const char* A, const char* B, uint64_t m, uint64_t n, uint64_t w, double g, double h,
+                   int32_t* Hout, double* score) {
+  if ((m > n ? m - n : n - m) > w) return ORC_ERR_ARG;
+  const double NI = -INFINITY;
+  const uint64_t W = n + 1;
+  double *p1 = malloc(sizeof(double) * W), *p2 = malloc(sizeof(double) * W), *p3 = malloc(sizeof(double) * W);
+  double *c1 = malloc(sizeof(double) * W), *c2 = malloc(sizeof(double) * W), *c3 = malloc(sizeof(double) * W);
+  if (!p1 || !p2 || !p3 || !c1 || !c2 || !c3) return ORC_ERR_NOMEM;
+  p1[0] = 0; p2[0] = NI; p3[0] = NI;
+  for (uint64_t j = 1; j <= n; j++) { p1[j] = NI; p3[j] = NI; p2[j] = (j <= w) ? -h - g * (double)j : NI; }
+  if (Hout) memset(Hout, 0, sizeof(int32_t) * (m + 1) * W);
+  for (uint64_t i = 1; i <= m; i++) {
+    for (uint64_t j = 0; j <= n; j++) { c1[j] = NI; c2[j] = NI; c3[j] = NI; }
+    if (i <= w) c3[0] = -h - g * (double)i;
+    const uint64_t jlo = (i > w) ? i - w : 1;
+    const uint64_t jhi = (i + w < n) ? i + w : n;
+    for (uint64_t j = jlo; j <= jhi; j++) {
+      const double f = (A[i - 1] == B[j - 1]) ? 1.0 : 0.0;
+      c1[j] = f + dmax(dmax(p1[j - 1], p2[j - 1]), p3[j - 1]);
+      c3[j] = dmax(dmax(p1[j] - g - h, p2[j] - g - h), p3[j] - g);
+      c2[j] = dmax(dmax(c1[j - 1] - g - h, c2[j - 1] - g), c3[j - 1] - g - h);
+      if (Hout) Hout[i * W + j] = (int32_t)dmax(dmax(c1[j], c2[j]), c3[j]);
+    }
+    double* t;
+    t = p1; p1 = c1; c1 = t;
+    t = p2; p2 = c2; c2 = t;
+    t = p3; p3 = c3; c3 = t;
+  }
+  *score = dmax(dmax(p1[n], p2[n]), p3[n]);
+  free(p1); free(p2); free(p3); free(c1); free(c2); free(c3);
+  return ORC_OK;
+}
+
+/* ---------------------------------------------------------------------------
+ * Order-independent digest of the interior of an int32 matrix: sum over
+ * i in [1,m], j in [1,n] (optionally only |i-j| <= w) of
+ *   mix(i,j) * (uint32)H(i,j)  mod 2^64,  mix = splitmix64(i<<32 | j) | 1.
+ * The GPU computes the same digest on its own layout.
+ * ------------------------------------------------------------------------- */
+static inline uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+uint64_t orc_mix(uint64_t i, uint64_t j) { return splitmix64((i << 32) | j) | 1ull; }
+
+uint64_t orc_checksum_h(const int32_t* H, uint64_t m, uint64_t n, uint64_t stride, int64_t w) {
+  uint64_t acc = 0;
+  for (uint64_t i = 1; i <= m; i++)
+    for (uint64_t j = 1; j <= n; j++) {
+      if (w >= 0) {
+        const int64_t d = (int64_t)i - (int64_t)j;
+        if (d > w || -d > w) continue;
+      }
+      acc += orc_mix(i, j) * (uint64_t)(uint32_t)H[i * stride + j];
+    }
+  return acc;
+}

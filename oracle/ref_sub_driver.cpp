@@ -1,0 +1,67 @@
+// ref_sub_driver.cpp -- TEST INFRASTRUCTURE ONLY (oracle/_ref).
+//
+// A thin extern "C" driver around the reference's own, unmodified
+// alignment_algorithm/subproblem_alignment.{h,cpp}, which oracle/Makefile
+// compiles straight from /root/reference.  Used to generate golden fixtures
+// (tests/golden/make_golden.py), to cross-check the C restatement
+// (oracle/msa_oracle.c), and as bench.py's "reference" CPU baseline.
+// main_alignment.cpp does not compile as shipped (wrong include at
+// main_alignment.cpp:6-7, conflict marker at :405), so it is NOT built; its
+// single-subproblem glue is restated in msa_oracle.c:orc_main_alignment.
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+
+#include "subproblem_alignment.h"
+
+extern "C" {
+
+// Runs Subproblem(A,B,m,n,idA,idB,p,start,end,g,h).compute_tables() (the
+// parallel row sweep, subproblem_alignment.cpp:329) and, if nodes_cap > 0,
+// find_alignment() (:105).  Tables are copied out row-major when T1 != NULL
+// ((m'+1) x (n'+1), m' = min(m,n) after the constructor's swap).
+int ref_subproblem(const char* A, const char* B, size_t m, size_t n, size_t idA, size_t idB, size_t p,
+                   int start_type, int end_type, double g, double h, double* T1, double* T2, double* T3,
+                   int* invert, size_t nodes_cap, size_t* n_nodes, unsigned long long* nodes_i,
+                   unsigned long long* nodes_j, int* nodes_t, unsigned long long* end_node, double* fill_seconds) {
+  Subproblem sp(const_cast<char*>(A), const_cast<char*>(B), m, n, idA, idB, p, start_type, end_type, g, h);
+  auto t0 = std::chrono::steady_clock::now();
+  sp.compute_tables();
+  auto t1 = std::chrono::steady_clock::now();
+  if (fill_seconds) *fill_seconds = std::chrono::duration<double>(t1 - t0).count();
+  *invert = sp.invert ? 1 : 0;
+  if (T1) {
+    const size_t W = sp.n + 1;
+    for (size_t i = 0; i <= sp.m; i++) {
+      std::memcpy(T1 + i * W, sp.T1[i].data(), sizeof(double) * W);
+      std::memcpy(T2 + i * W, sp.T2[i].data(), sizeof(double) * W);
+      std::memcpy(T3 + i * W, sp.T3[i].data(), sizeof(double) * W);
+    }
+  }
+  if (nodes_cap > 0) {
+    sp.find_alignment();
+    size_t k = 0;
+    for (align* a = sp.alignment_begin; a != NULL; a = a->next, k++) {
+      if (k < nodes_cap) {
+        nodes_i[k] = a->i;
+        nodes_j[k] = a->j;
+        nodes_t[k] = a->t;
+      }
+    }
+    *n_nodes = k;
+    end_node[0] = sp.alignment_end->i;
+    end_node[1] = sp.alignment_end->j;
+    end_node[2] = (unsigned long long)(long long)sp.alignment_end->t;
+    // the reference leaks these; free them here
+    align* a = sp.alignment_begin;
+    while (a != NULL) {
+      align* nx = a->next;
+      std::free(a);
+      a = nx;
+    }
+    if (sp.alignment_begin == NULL) std::free(sp.alignment_end);
+  }
+  return 0;
+}
+
+}  // extern "C"
