@@ -1,0 +1,406 @@
+// msa_capi.hip -- host side of the C-ABI (include/msa.h): plans, launches,
+// and the reference-compatible entry points.  All DP cells are computed by the
+// kernels in msa_kernels.hip; the host only encodes inputs, de-skews outputs
+// and walks traceback bits (O(m+n), like the reference's find_alignment).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/msa.h"
+#include "msa_kernels.hip"
+
+using namespace msa;
+
+namespace {
+
+#define HIPCHK(x)                                         \
+  do {                                                    \
+    hipError_t e_ = (x);                                  \
+    if (e_ != hipSuccess) {                               \
+      std::fprintf(stderr, "msa: %s failed: %s\n", #x, hipGetErrorString(e_)); \
+      return MSA_ERR_HIP;                                 \
+    }                                                     \
+  } while (0)
+
+int g_dev_checked = 0;
+int g_dev_ok = 0;
+std::mutex g_dev_mu;
+
+int ensure_device() {
+  std::lock_guard<std::mutex> lk(g_dev_mu);
+  if (!g_dev_checked) {
+    g_dev_checked = 1;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+      g_dev_ok = 0;
+    } else {
+      hipDeviceProp_t prop;
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      g_dev_ok = (hipGetDeviceProperties(&prop, dev) == hipSuccess) &&
+                 (std::strncmp(prop.gcnArchName, "gfx950", 6) == 0);
+      if (!g_dev_ok) std::fprintf(stderr, "msa: device 0 is %s, need gfx950\n", prop.gcnArchName);
+    }
+  }
+  return g_dev_ok ? MSA_OK : MSA_ERR_NODEV;
+}
+
+int nc_of(int alg) {
+  switch (alg) {
+    case MSA_ALG_SWL: return 1;
+    case MSA_ALG_SWA: case MSA_ALG_NWA: return 2;
+    default: return 3;
+  }
+}
+
+typedef void (*kfn_t)(KArgs);
+
+template <int ALG, int OUT, bool TP>
+kfn_t kf() { return stripe_kernel<ALG, OUT, TP>; }
+
+kfn_t pick_kernel(int alg, int out, int tp) {
+#define K3(A, O) return tp ? kf<A, O, true>() : kf<A, O, false>()
+  switch (alg) {
+    case MSA_ALG_SWL:
+      if (out == MSA_OUT_NONE) K3(MSA_ALG_SWL, MSA_OUT_NONE);
+      if (out == MSA_OUT_H) K3(MSA_ALG_SWL, MSA_OUT_H);
+      break;
+    case MSA_ALG_SWA:
+      if (out == MSA_OUT_NONE) K3(MSA_ALG_SWA, MSA_OUT_NONE);
+      if (out == MSA_OUT_H) K3(MSA_ALG_SWA, MSA_OUT_H);
+      if (out == MSA_OUT_DIR) K3(MSA_ALG_SWA, MSA_OUT_DIR);
+      break;
+    case MSA_ALG_NWA:
+      if (out == MSA_OUT_NONE) return kf<MSA_ALG_NWA, MSA_OUT_NONE, false>();
+      if (out == MSA_OUT_H) return kf<MSA_ALG_NWA, MSA_OUT_H, false>();
+      break;
+    case MSA_ALG_REF:
+      if (out == MSA_OUT_NONE) return kf<MSA_ALG_REF, MSA_OUT_NONE, false>();
+      if (out == MSA_OUT_TAB) return kf<MSA_ALG_REF, MSA_OUT_TAB, false>();
+      if (out == MSA_OUT_DIR) return kf<MSA_ALG_REF, MSA_OUT_DIR, false>();
+      if (out == MSA_OUT_H) return kf<MSA_ALG_REF, MSA_OUT_H, false>();
+      break;
+    case MSA_ALG_PART:
+      if (out == MSA_OUT_TAB) return kf<MSA_ALG_PART, MSA_OUT_TAB, false>();
+      break;
+  }
+#undef K3
+  return nullptr;
+}
+
+}  // namespace
+
+struct msa_plan {
+  msa_plan_desc d;
+  msa_kparams kp;
+  int nc = 1;
+  std::vector<msa_pair_desc> pairs;
+  int64_t total_stripes = 0;
+  int64_t cells_elems = 0;
+  size_t lds_bytes = 0;
+  int grid = 1;
+  int gbuf_stride = 0;
+  kfn_t fn = nullptr;
+  // device
+  msa_pair_desc* d_pairs = nullptr;
+  msa_stripe_meta* d_meta = nullptr;
+  int* d_ticket = nullptr;  // [0] ticket, [1] err
+  unsigned long long* d_gbuf = nullptr;
+  PairResult* d_res = nullptr;
+  unsigned long long* d_sum = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  uint32_t epoch = 0;
+};
+
+extern "C" {
+
+const char* msa_status_string(int s) {
+  switch (s) {
+    case MSA_OK: return "ok";
+    case MSA_ERR_ARG: return "invalid argument";
+    case MSA_ERR_ALPHABET: return "more than 8 distinct symbols";
+    case MSA_ERR_HIP: return "HIP runtime error";
+    case MSA_ERR_NODEV: return "no gfx950 device";
+    case MSA_ERR_UNSUPPORTED: return "unsupported parameters (GPU path needs integral g,h)";
+    case MSA_ERR_TIMEOUT: return "cross-workgroup wait timed out";
+    case MSA_ERR_NOMEM: return "out of memory";
+    case MSA_ERR_CAPACITY: return "output buffer too small";
+    case MSA_ERR_NOMATCH: return "traceback found no predecessor";
+  }
+  return "unknown status";
+}
+
+int msa_version(void) { return 1; }
+
+int msa_device_count(int* count) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  if (count) *count = n;
+  return n > 0 ? MSA_OK : MSA_ERR_NODEV;
+}
+
+int msa_encode_pair(const char* A0, size_t m, const char* B0, size_t n, uint8_t* ca, uint8_t* cb) {
+  int map[256];
+  for (int k = 0; k < 256; ++k) map[k] = -1;
+  int next = 0;
+  auto enc = [&](const char* s, size_t len, uint8_t* out) -> int {
+    for (size_t k = 0; k < len; ++k) {
+      const unsigned char c = (unsigned char)s[k];
+      if (map[c] < 0) {
+        if (next >= 8) return MSA_ERR_ALPHABET;
+        map[c] = next++;
+      }
+      out[k] = (uint8_t)map[c];
+    }
+    return MSA_OK;
+  };
+  // DNA fast path: fixed codes so batches share one code map
+  const char* dna = "ACGT";
+  for (int k = 0; k < 4; ++k) map[(unsigned char)dna[k]] = k;
+  next = 4;
+  int rc = enc(A0, m, ca);
+  if (rc != MSA_OK) return rc;
+  return enc(B0, n, cb);
+}
+
+int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
+  if (!desc || !out || desc->n_pairs <= 0 || !desc->m || !desc->n || !desc->a_off || !desc->b_off) return MSA_ERR_ARG;
+  int rc = ensure_device();
+  if (rc != MSA_OK) return rc;
+  msa_plan* P = new (std::nothrow) msa_plan();
+  if (!P) return MSA_ERR_NOMEM;
+  P->d = *desc;
+  P->d.m = P->d.n = P->d.a_off = P->d.b_off = nullptr;
+  const int alg = desc->alg;
+  int out_mode = desc->cells;
+  int kalg;
+  switch (alg) {
+    case MSA_SW_LINEAR: kalg = MSA_ALG_SWL; break;
+    case MSA_SW_AFFINE: kalg = MSA_ALG_SWA; break;
+    case MSA_NW_BANDED: kalg = MSA_ALG_NWA; break;
+    case MSA_REF_GOTOH: kalg = MSA_ALG_REF; break;
+    case MSA_PARTIAL: kalg = MSA_ALG_PART; break;
+    default: delete P; return MSA_ERR_ARG;
+  }
+  const int tp = (kalg == MSA_ALG_SWL || kalg == MSA_ALG_SWA) ? (desc->track_end ? 1 : 0) : 0;
+  P->fn = pick_kernel(kalg, out_mode, tp);
+  if (!P->fn) { delete P; return MSA_ERR_UNSUPPORTED; }
+  if (desc->single && desc->n_pairs != 1) { delete P; return MSA_ERR_ARG; }
+  P->nc = nc_of(kalg);
+  const int band = (kalg == MSA_ALG_NWA) ? desc->band : -1;
+  msa_kparams& kp = P->kp;
+  std::memset(&kp, 0, sizeof(kp));
+  kp.alg = kalg;
+  kp.out = out_mode;
+  kp.match = desc->match;
+  kp.mismatch = desc->mismatch;
+  kp.gap_open = desc->gap_open;
+  kp.gap_ext = desc->gap_extend;
+  if (kalg == MSA_ALG_SWL) kp.gap_open = kp.gap_ext = desc->gap_extend;
+  kp.h = desc->gap_open - desc->gap_extend;
+  kp.start_type = desc->start_type;
+  kp.band = band;
+  kp.single = desc->single ? 1 : 0;
+  kp.n_pairs = (int)desc->n_pairs;
+  if (kalg == MSA_ALG_NWA && kp.h < 0) { delete P; return MSA_ERR_UNSUPPORTED; }
+  // geometry
+  int64_t stripe0 = 0, off = 0;
+  int max_S = 0, max_P = 0, max_code = 0;
+  P->pairs.resize(desc->n_pairs);
+  for (int64_t p = 0; p < desc->n_pairs; ++p) {
+    const int64_t m = desc->m[p], n = desc->n[p];
+    if (m <= 0 || n <= 0 || m > (1 << 26) || n > (1 << 26)) { delete P; return MSA_ERR_ARG; }
+    if (band >= 0 && std::llabs(m - n) > band) { delete P; return MSA_ERR_ARG; }
+    const int S = (int)((m + 63) / 64);
+    int pmax = 0;
+    // per-item code window (items = groups of 8 in single mode, whole pair in batch)
+    const int per_item = desc->single ? MSA_WAVES : S;
+    for (int k0 = 0; k0 < S; k0 += per_item) {
+      int cmin = 1 << 30, cmax = -(1 << 30);
+      for (int k = k0; k < std::min(S, k0 + per_item); ++k) {
+        StripeGeom g;
+        stripe_geom(k, (int)m, (int)n, band, g);
+        pmax = std::max(pmax, g.P);
+        cmin = std::min(cmin, g.cs - 64);
+        cmax = std::max(cmax, g.cs + g.P * MSA_K);
+      }
+      cmin &= ~3;
+      max_code = std::max(max_code, cmax - cmin + 8);
+    }
+    msa_pair_desc& pd = P->pairs[p];
+    pd.a_off = desc->a_off[p];
+    pd.b_off = desc->b_off[p];
+    pd.m = (int)m;
+    pd.n = (int)n;
+    pd.stripe0 = (int)stripe0;
+    pd.pmax = pmax;
+    pd.out_off = off;
+    const int64_t cells = (int64_t)S * pmax * MSA_K * 64;
+    off += (cells + 63) & ~int64_t(63);
+    stripe0 += S;
+    max_S = std::max(max_S, S);
+    max_P = std::max(max_P, pmax);
+  }
+  P->total_stripes = stripe0;
+  P->cells_elems = off;
+  kp.sched_cap = desc->single ? MSA_WAVES : max_S;
+  kp.lds_code_bytes = ((max_code + 16) + 15) & ~15;
+  kp.lds_row_words = desc->single ? 0 : (((max_P * MSA_K + MSA_ROWOFF + 32) + 15) & ~15);
+  if (desc->single) {
+    const int S = (int)((desc->m[0] + 63) / 64);
+    kp.n_items = (S + MSA_WAVES - 1) / MSA_WAVES;
+  } else {
+    kp.n_items = (int)desc->n_pairs;
+  }
+  const size_t lds_ints = 16 + (size_t)kp.sched_cap * 8 + (size_t)(MSA_WAVES + 1) * P->nc * MSA_RING +
+                          (size_t)P->nc * kp.lds_row_words + (size_t)kp.lds_code_bytes;  // 4 copies = bytes*4/4
+  P->lds_bytes = lds_ints * 4;
+  if (P->lds_bytes > 160 * 1024) {
+    std::fprintf(stderr, "msa: problem needs %zu B of LDS per workgroup (> 160 KiB)\n", P->lds_bytes);
+    delete P;
+    return MSA_ERR_UNSUPPORTED;
+  }
+  if (hipFuncSetAttribute((const void*)P->fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P->lds_bytes) !=
+      hipSuccess) {
+    delete P;
+    return MSA_ERR_HIP;
+  }
+  int occ = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)P->fn, 512, P->lds_bytes) != hipSuccess || occ < 1)
+    occ = 1;
+  hipDeviceProp_t prop;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipGetDeviceProperties(&prop, dev);
+  const int cap = prop.multiProcessorCount * std::min(occ, 2);
+  P->grid = std::max(1, std::min(kp.n_items, cap));
+  // device buffers
+  auto fail = [&](void) { msa_plan_destroy(P); return MSA_ERR_HIP; };
+  if (hipMalloc(&P->d_pairs, sizeof(msa_pair_desc) * P->pairs.size()) != hipSuccess) return fail();
+  if (hipMemcpy(P->d_pairs, P->pairs.data(), sizeof(msa_pair_desc) * P->pairs.size(), hipMemcpyHostToDevice) !=
+      hipSuccess)
+    return fail();
+  if (hipMalloc(&P->d_meta, sizeof(msa_stripe_meta) * std::max<int64_t>(1, P->total_stripes)) != hipSuccess)
+    return fail();
+  if (hipMemset(P->d_meta, 0, sizeof(msa_stripe_meta) * std::max<int64_t>(1, P->total_stripes)) != hipSuccess)
+    return fail();
+  if (hipMalloc(&P->d_ticket, 64) != hipSuccess) return fail();
+  if (hipMalloc(&P->d_res, sizeof(PairResult) * desc->n_pairs) != hipSuccess) return fail();
+  if (hipMalloc(&P->d_sum, 64) != hipSuccess) return fail();
+  if (desc->single && kp.n_items > 1) {
+    P->gbuf_stride = (int)(((desc->n[0] + 2 * MSA_GOFF + 16) + 15) & ~15);
+    const size_t gb = (size_t)(kp.n_items - 1) * P->nc * P->gbuf_stride * sizeof(unsigned long long);
+    if (hipMalloc(&P->d_gbuf, gb) != hipSuccess) return fail();
+    if (hipMemset(P->d_gbuf, 0, gb) != hipSuccess) return fail();
+  }
+  if (hipEventCreate(&P->ev0) != hipSuccess || hipEventCreate(&P->ev1) != hipSuccess) return fail();
+  *out = P;
+  return MSA_OK;
+}
+
+void msa_plan_destroy(msa_plan* P) {
+  if (!P) return;
+  if (P->d_pairs) (void)hipFree(P->d_pairs);
+  if (P->d_meta) (void)hipFree(P->d_meta);
+  if (P->d_ticket) (void)hipFree(P->d_ticket);
+  if (P->d_gbuf) (void)hipFree(P->d_gbuf);
+  if (P->d_res) (void)hipFree(P->d_res);
+  if (P->d_sum) (void)hipFree(P->d_sum);
+  if (P->ev0) (void)hipEventDestroy(P->ev0);
+  if (P->ev1) (void)hipEventDestroy(P->ev1);
+  delete P;
+}
+
+int msa_plan_cells_size(const msa_plan* P, int64_t* elems) {
+  if (!P || !elems) return MSA_ERR_ARG;
+  *elems = (P->d.cells == MSA_CELLS_NONE) ? 0 : P->cells_elems;
+  return MSA_OK;
+}
+
+int64_t msa_plan_stripes(const msa_plan* P) { return P ? P->total_stripes : 0; }
+
+int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, void* c1, void* c2, void* stream) {
+  if (!P || !dA || !dB) return MSA_ERR_ARG;
+  if (P->d.cells != MSA_CELLS_NONE && !c0) return MSA_ERR_ARG;
+  if (P->d.cells == MSA_CELLS_TAB && (!c1 || !c2)) return MSA_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  KArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.kp = P->kp;
+  if (++P->epoch == 0) P->epoch = 1;
+  a.kp.epoch = P->epoch;
+  a.A = dA;
+  a.B = dB;
+  a.pairs = P->d_pairs;
+  a.meta = P->d_meta;
+  a.ticket = P->d_ticket;
+  a.err = P->d_ticket + 1;
+  a.gbuf = P->d_gbuf;
+  a.gbuf_stride = P->gbuf_stride;
+  if (P->d.cells == MSA_CELLS_DIR) a.outDir = (uint8_t*)c0;
+  else a.outH = (int32_t*)c0;
+  a.outT2 = (int32_t*)c1;
+  a.outT3 = (int32_t*)c2;
+  HIPCHK(hipMemsetAsync(P->d_ticket, 0, 64, st));
+  HIPCHK(hipEventRecord(P->ev0, st));
+  hipLaunchKernelGGL(P->fn, dim3(P->grid), dim3(512), P->lds_bytes, st, a);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(P->ev1, st));
+  const int sw = (P->kp.alg == MSA_ALG_SWL || P->kp.alg == MSA_ALG_SWA) ? 1 : 0;
+  const int np = (int)P->d.n_pairs;
+  hipLaunchKernelGGL(reduce_pairs_kernel, dim3((np + 255) / 256), dim3(256), 0, st, P->d_pairs, P->d_meta, np, sw,
+                     P->d_res);
+  HIPCHK(hipGetLastError());
+  return MSA_OK;
+}
+
+int msa_plan_last_kernel_ms(msa_plan* P, float* ms) {
+  if (!P || !ms) return MSA_ERR_ARG;
+  HIPCHK(hipEventSynchronize(P->ev1));
+  HIPCHK(hipEventElapsedTime(ms, P->ev0, P->ev1));
+  return MSA_OK;
+}
+
+int msa_plan_results(msa_plan* P, msa_pair_result* out, void* stream) {
+  if (!P || !out) return MSA_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  int err[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(err, P->d_ticket, sizeof(err), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(out, P->d_res, sizeof(PairResult) * P->d.n_pairs, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  static_assert(sizeof(PairResult) == sizeof(msa_pair_result), "result layout");
+  if (err[1]) return MSA_ERR_TIMEOUT;
+  return MSA_OK;
+}
+
+int msa_plan_stripe_meta(msa_plan* P, int32_t* out, int64_t cap, void* stream) {
+  if (!P || !out || cap < P->total_stripes) return MSA_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  static_assert(sizeof(msa_stripe_meta) == 12 * 4, "meta layout");
+  HIPCHK(hipMemcpyAsync(out, P->d_meta, sizeof(msa_stripe_meta) * P->total_stripes, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  return MSA_OK;
+}
+
+int msa_plan_checksum(msa_plan* P, const int32_t* dH, int64_t pair, uint64_t* digest, void* stream) {
+  if (!P || !dH || !digest || pair < 0 || pair >= P->d.n_pairs) return MSA_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  HIPCHK(hipMemsetAsync(P->d_sum, 0, 8, st));
+  hipLaunchKernelGGL(checksum_kernel, dim3(1024), dim3(256), 0, st, dH, P->d_pairs, P->d_meta, (int)pair,
+                     P->kp.band, P->d_sum);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(digest, P->d_sum, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  return MSA_OK;
+}
+
+}  // extern "C"
+#include "msa_refapi.inc"

@@ -1,0 +1,868 @@
+// msa_kernels.hip -- the DP-fill hot path as hand-written CDNA4 (gfx950) HIP.
+//
+// Replaces the reference's row sweep (Subproblem::compute_tables,
+// subproblem_alignment.cpp:329-332; per-row T1/T3 map :229-235, T2 via the
+// omega + ParallelPrefixMax scan :237-249 / :13-103) and partial.cpp's
+// forward/reverse fills (:53-79) with ONE templated anti-diagonal stripe
+// wavefront kernel:
+//
+//  * A "stripe" is 64 consecutive DP rows; one wave64 owns it, lane r = row
+//    64s+r+1.  At step t lane r processes column cs + t - r (cs = the stripe's
+//    start column), so the wave sweeps an anti-diagonal band.  The left
+//    dependence stays in-lane (registers); the up/diag dependence comes from
+//    lane r-1 through one DPP `wave_shr:1` per carried value (no LDS, no
+//    __shfl).  The reference's horizontal prefix-max scan is not needed: the
+//    in-lane left carry IS the scan.
+//  * Lane 0 receives the row above the stripe as dedicated registers (DPP
+//    `old` operand), lane 63 hands its bottom row to the next stripe through
+//    an LDS ring (same workgroup) or 8-byte {tag,value} granules in HBM
+//    (next workgroup; tag = launch epoch, so the data is its own flag).
+//  * 8 waves per workgroup run 8 stripes in lock-step phases of 16 steps
+//    (one s_barrier per phase); stripe k starts D_k ~ 5 phases after k-1.
+//  * The substitution score comes from a per-lane 8-byte profile selected by
+//    v_perm_b32 with 4 column codes at a time; the byte is sign-extended into
+//    the diagonal add by SDWA (no separate extract).
+//  * Outputs (H / traceback bits / T1,T2,T3) are written in a skewed stripe
+//    layout: one global_store_dwordx4 per lane per 4 steps, fully coalesced
+//    (1 KiB per wave instruction).  Layout: element (s, t, r) of pair block
+//    = ((s * pmax*4 + t/4) * 64 + r) * 4 + t%4   <->   cell (64s+r+1, cs_s+t-r).
+//
+// Two launch modes share the kernel:
+//  * single: one pair, items = groups of 8 stripes, tickets in order
+//    (a workgroup only ever waits on an earlier ticket -> no deadlock).
+//  * batch: items = whole pairs; wave w runs stripes w, w+8, ...; the
+//    wave 7 -> wave 0 wrap link goes through a full LDS row buffer.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "msa_types.h"
+
+#define MSA_WAVES 8
+#define MSA_K 16
+#define MSA_RING 512
+#define MSA_ROWOFF 128
+#define MSA_GOFF 128
+#define MSA_NEG (-(1 << 30))
+
+namespace msa {
+
+template <int ALG> struct Tr;
+template <> struct Tr<MSA_ALG_SWL> { static constexpr int NC = 1; };
+template <> struct Tr<MSA_ALG_SWA> { static constexpr int NC = 2; };
+template <> struct Tr<MSA_ALG_NWA> { static constexpr int NC = 2; };
+template <> struct Tr<MSA_ALG_REF> { static constexpr int NC = 3; };
+template <> struct Tr<MSA_ALG_PART> { static constexpr int NC = 3; };
+
+__device__ __forceinline__ int dpp_shr1(int old, int src) {
+  return __builtin_amdgcn_update_dpp(old, src, 0x138, 0xf, 0xf, false);
+}
+__host__ __device__ __forceinline__ int imax(int a, int b) { return a > b ? a : b; }
+__device__ __forceinline__ int imax3(int a, int b, int c) { return imax(imax(a, b), c); }
+// first index (1,2,3) attaining the max, the reference's tie order
+// (subproblem_alignment.cpp:130-145, partial.cpp:153)
+__device__ __forceinline__ int firstmax3(int a, int b, int c) {
+  return (a >= b && a >= c) ? 1 : (b >= c ? 2 : 3);
+}
+__device__ __forceinline__ int wrap_add(int a, int b) { return (int)((unsigned)a + (unsigned)b); }
+__device__ __forceinline__ int wrap_sub(int a, int b) { return (int)((unsigned)a - (unsigned)b); }
+
+struct StripeGeom {
+  int T, P, cs, lead, mask_lo, mask_hi, c_hi, pad;
+};
+
+__host__ __device__ __forceinline__ int jlo_of(int i, int band) { return band < 0 ? 1 : imax(1, i - band); }
+__host__ __device__ __forceinline__ int jhi_of(int i, int n, int band) { return band < 0 ? n : (i + band < n ? i + band : n); }
+
+// Geometry of pair-local stripe k (rows 64k+1 .. 64k+64).
+__host__ __device__ inline void stripe_geom(int k, int m, int n, int band, StripeGeom& g) {
+  const int i0 = 64 * k + 1;
+  const int rlast = (m - 64 * k - 1 < 63) ? (m - 64 * k - 1) : 63;
+  const int ilast = i0 + rlast;
+  const int clo = jlo_of(i0, band);
+  int lead = (clo - 1 - k) % 16;
+  if (lead < 0) lead += 16;
+  lead += 1;
+  g.lead = lead;
+  g.cs = clo - lead;
+  const int tmax_max = jhi_of(ilast, n, band) - g.cs + rlast;
+  g.P = tmax_max / MSA_K + 1;
+  g.mask_lo = jlo_of(ilast, band) - g.cs + rlast;  // max over rows of tmin
+  g.mask_hi = jhi_of(i0, n, band) - g.cs;          // min over rows of tmax
+  g.c_hi = jhi_of(ilast, n, band);
+  g.T = 0;
+  g.pad = 0;
+}
+
+struct KArgs {
+  msa_kparams kp;
+  const uint8_t* A;
+  const uint8_t* B;
+  const msa_pair_desc* pairs;
+  msa_stripe_meta* meta;
+  int* ticket;
+  unsigned long long* gbuf;  // single mode: [n_items-1][NC][n + 2*GOFF] granules
+  int gbuf_stride;           // granules per (item, value)
+  int* err;                  // timeout / error flag
+  int32_t* outH;             // O_H (or plane 0 of O_TAB)
+  int32_t* outT2;            // O_TAB planes
+  int32_t* outT3;
+  uint8_t* outDir;           // O_DIR
+};
+
+template <int ALG>
+__device__ __forceinline__ void border_top(const msa_kparams& kp, int c, int (&v)[3]) {
+  // Row 0 of the DP at column c (c may be < 0: unused, return NEG).
+  if constexpr (ALG == MSA_ALG_SWL || ALG == MSA_ALG_SWA) {
+    v[0] = c >= 0 ? 0 : MSA_NEG;  // H
+    v[1] = MSA_NEG;               // F
+    v[2] = MSA_NEG;
+  } else if constexpr (ALG == MSA_ALG_NWA) {
+    // H(0,c) = max(T1,T2,T3)(0,c): 0 at c=0, -h-g*c for 1<=c<=band; F = -inf
+    const bool inb = (kp.band < 0) || (c <= kp.band);
+    v[0] = (c == 0) ? 0 : ((c > 0 && inb) ? -kp.h - kp.gap_ext * c : MSA_NEG);
+    v[1] = MSA_NEG;
+    v[2] = MSA_NEG;
+  } else if constexpr (ALG == MSA_ALG_REF) {
+    // compute_row(0) / ComputeFirstRowMapThread (subproblem_alignment.cpp:212-227,259-280)
+    const int st = kp.start_type;
+    const int g = kp.gap_ext, h = kp.h;
+    if (c < 0) { v[0] = v[1] = v[2] = MSA_NEG; return; }
+    if (c == 0) {
+      v[0] = (st == 1 || st == -1) ? 0 : MSA_NEG;
+      v[1] = (st == -2) ? 0 : MSA_NEG;
+      v[2] = (st == -3) ? 0 : MSA_NEG;
+    } else {
+      v[0] = MSA_NEG;
+      v[2] = MSA_NEG;
+      v[1] = (st == -2) ? -g * c : ((st == 1 || st == 3) ? MSA_NEG : -h - g * c);
+    }
+  } else {  // PART: initializeTables (partial.cpp:13-31), wrap semantics
+    const int st = kp.start_type;
+    v[0] = (c == 0 && st == 1) ? 0 : INT32_MIN;
+    v[1] = (c >= 1 && st == 2) ? (int)((unsigned)(-kp.gap_open) * (unsigned)c) : INT32_MIN;
+    v[2] = INT32_MIN;
+  }
+}
+
+template <int ALG>
+__device__ __forceinline__ void border_left(const msa_kparams& kp, int i, int (&v)[3]) {
+  // Column 0 of row i (i >= 1), state order of each algorithm.
+  if constexpr (ALG == MSA_ALG_SWL || ALG == MSA_ALG_SWA) {
+    v[0] = 0;        // H
+    v[1] = MSA_NEG;  // E
+    v[2] = MSA_NEG;  // F
+  } else if constexpr (ALG == MSA_ALG_NWA) {
+    const bool inb = (kp.band < 0) || (i <= kp.band);
+    v[0] = inb ? -kp.h - kp.gap_ext * i : MSA_NEG;  // H
+    v[1] = MSA_NEG;                                 // T2 (E)
+    v[2] = v[0];                                    // T3 (F) = -h-g*i
+  } else if constexpr (ALG == MSA_ALG_REF) {
+    // compute_row(i>0) borders (subproblem_alignment.cpp:282-292)
+    const int st = kp.start_type;
+    v[0] = MSA_NEG;
+    v[1] = MSA_NEG;
+    v[2] = (st == -3) ? -kp.gap_ext * i : ((st == 1 || st == 2) ? MSA_NEG : -kp.h - kp.gap_ext * i);
+  } else {
+    const int st = kp.start_type;
+    v[0] = INT32_MIN;
+    v[1] = INT32_MIN;
+    v[2] = (st == 3) ? (int)((unsigned)(-kp.gap_open) * (unsigned)i) : INT32_MIN;
+  }
+}
+
+// Per-lane register state of the stripe a wave is running.
+template <int ALG>
+struct LaneState {
+  int S[3];    // left-cell state (algorithm order, see step())
+  int U[3];    // diagonal values (previous step's up values)
+  int LB[3];   // left border held while t < tmin
+  int tmin, tmax;
+  int best, bt;  // SW best in this lane's row and the step it first occurred
+  int fin[3];
+  unsigned plo, phi;  // substitution profile (8 int8 scores by column code)
+  int i;              // DP row
+  int cw_base;        // LDS dword index base of this lane's code stream (copy cw_copy)
+  int cw_copy;
+};
+
+// One DP step for every lane.  in[v] = value lane 0 takes from the row above.
+// Returns the direction byte for O_DIR.
+template <int ALG, int OUT, bool MASKED, bool TRACKPOS>
+__device__ __forceinline__ unsigned step(const msa_kparams& kp, LaneState<ALG>& L, const int (&in)[3], int s,
+                                         int t, int (&carry)[3]) {
+  unsigned dir = 0;
+  int nS[3];
+  if constexpr (ALG == MSA_ALG_SWL) {
+    const int up = dpp_shr1(in[0], L.S[0]);
+    const int d = L.U[0] + s;
+    const int e = imax(up, L.S[0]) - kp.gap_open;
+    nS[0] = imax3(d, e, 0);
+    L.U[0] = up;
+  } else if constexpr (ALG == MSA_ALG_SWA) {
+    const int upH = dpp_shr1(in[0], L.S[0]);
+    const int upF = dpp_shr1(in[1], L.S[2]);
+    const int f = imax(upF - kp.gap_ext, upH - kp.gap_open);
+    const int e = imax(L.S[1] - kp.gap_ext, L.S[0] - kp.gap_open);
+    const int d = L.U[0] + s;
+    const int h = imax(imax3(d, e, f), 0);
+    if constexpr (OUT == MSA_OUT_DIR) {
+      const unsigned hs = (h == 0) ? 0u : (h == d ? 1u : (h == e ? 2u : 3u));
+      const unsigned eb = (e == L.S[0] - kp.gap_open) ? 4u : 0u;
+      const unsigned fb = (f == upH - kp.gap_open) ? 8u : 0u;
+      dir = hs | eb | fb;
+    }
+    nS[0] = h;
+    nS[1] = e;
+    nS[2] = f;
+    L.U[0] = upH;
+  } else if constexpr (ALG == MSA_ALG_NWA) {
+    const int upH = dpp_shr1(in[0], L.S[0]);
+    const int upF = dpp_shr1(in[1], L.S[2]);
+    const int t3 = imax(upH - kp.gap_open, upF - kp.gap_ext);
+    const int t2 = imax(L.S[0] - kp.gap_open, L.S[1] - kp.gap_ext);
+    const int t1 = L.U[0] + s;
+    nS[0] = imax3(t1, t2, t3);
+    nS[1] = t2;
+    nS[2] = t3;
+    L.U[0] = upH;
+  } else if constexpr (ALG == MSA_ALG_REF) {
+    const int u0 = dpp_shr1(in[0], L.S[0]);
+    const int u1 = dpp_shr1(in[1], L.S[1]);
+    const int u2 = dpp_shr1(in[2], L.S[2]);
+    const int GH = kp.gap_open, G = kp.gap_ext;
+    // exact -inf: every stored value is finite (> -2^29) or exactly MSA_NEG
+    const int mx = imax3(L.U[0], L.U[1], L.U[2]);
+    const int t1 = (mx == MSA_NEG) ? MSA_NEG : mx + s;
+    const int a = imax(L.S[0] - GH, MSA_NEG), b = imax(L.S[1] - G, MSA_NEG), c = imax(L.S[2] - GH, MSA_NEG);
+    const int t2 = imax3(a, b, c);
+    const int a3 = imax(u0 - GH, MSA_NEG), b3 = imax(u1 - GH, MSA_NEG), c3 = imax(u2 - G, MSA_NEG);
+    const int t3 = imax3(a3, b3, c3);
+    if constexpr (OUT == MSA_OUT_DIR) {
+      dir = (unsigned)firstmax3(L.U[0], L.U[1], L.U[2]) | ((unsigned)firstmax3(a, b, c) << 2) |
+            ((unsigned)firstmax3(a3, b3, c3) << 4);
+    }
+    nS[0] = t1;
+    nS[1] = t2;
+    nS[2] = t3;
+    L.U[0] = u0;
+    L.U[1] = u1;
+    L.U[2] = u2;
+  } else {  // PART: fillTablesParallel (partial.cpp:53-65), int32 wrap
+    const int u0 = dpp_shr1(in[0], L.S[0]);
+    const int u1 = dpp_shr1(in[1], L.S[1]);
+    const int u2 = dpp_shr1(in[2], L.S[2]);
+    const int GH = kp.gap_open, G = kp.gap_ext;
+    nS[0] = imax3(wrap_add(L.U[0], s), wrap_add(L.U[1], s), wrap_add(L.U[2], s));
+    nS[1] = imax3(wrap_sub(L.S[0], GH), wrap_sub(L.S[1], G), wrap_sub(L.S[2], GH));
+    nS[2] = imax3(wrap_sub(u0, GH), wrap_sub(u1, GH), wrap_sub(u2, G));
+    L.U[0] = u0;
+    L.U[1] = u1;
+    L.U[2] = u2;
+  }
+  constexpr int NS = (ALG == MSA_ALG_SWL) ? 1 : 3;
+  if constexpr (MASKED) {
+    const bool before = t < L.tmin;
+    const bool after = t > L.tmax;
+#pragma unroll
+    for (int v = 0; v < NS; ++v) nS[v] = before ? L.LB[v] : (after ? MSA_NEG : nS[v]);
+    if constexpr (ALG == MSA_ALG_SWL || ALG == MSA_ALG_SWA) {
+      if (!before && !after) {
+        if constexpr (TRACKPOS) {
+          if (nS[0] > L.best) { L.best = nS[0]; L.bt = t; }
+        } else {
+          L.best = imax(L.best, nS[0]);
+        }
+      }
+    } else {
+      if (t == L.tmax) {
+#pragma unroll
+        for (int v = 0; v < 3; ++v) L.fin[v] = nS[v];
+      }
+    }
+  } else {
+    if constexpr (ALG == MSA_ALG_SWL || ALG == MSA_ALG_SWA) {
+      if constexpr (TRACKPOS) {
+        if (nS[0] > L.best) { L.best = nS[0]; L.bt = t; }
+      } else {
+        L.best = imax(L.best, nS[0]);
+      }
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < NS; ++v) L.S[v] = nS[v];
+  // carried values (what the lane below / next stripe needs)
+  if constexpr (ALG == MSA_ALG_SWL) {
+    carry[0] = nS[0];
+  } else if constexpr (ALG == MSA_ALG_SWA || ALG == MSA_ALG_NWA) {
+    carry[0] = nS[0];
+    carry[1] = nS[2];
+  } else {
+    carry[0] = nS[0];
+    carry[1] = nS[1];
+    carry[2] = nS[2];
+  }
+  return dir;
+}
+
+// Bounded spin helper for cross-workgroup granule waits.
+__device__ __forceinline__ unsigned long long gload(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gstore(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+enum Src { SRC_BORDER = 0, SRC_RING = 1, SRC_ROW = 2, SRC_GLOBAL = 3 };
+enum Snk { SNK_NONE = 0, SNK_RING = 1, SNK_ROW = 2, SNK_GLOBAL = 3 };
+
+template <int ALG, int OUT, bool TRACKPOS>
+__global__ __launch_bounds__(512) void stripe_kernel(KArgs a) {
+  constexpr int NC = Tr<ALG>::NC;
+  constexpr int W = MSA_WAVES;
+  extern __shared__ __attribute__((aligned(16))) int smem[];
+  const msa_kparams& kp = a.kp;
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+
+  // ---- LDS carve (int32 units, all offsets multiples of 4) ----
+  int* misc = smem;                                   // 16 ints
+  StripeGeom* sched = reinterpret_cast<StripeGeom*>(smem + 16);
+  const int sched_cap = kp.sched_cap;
+  int* rings = smem + 16 + sched_cap * 8;             // (W+1) x NC x RING
+  int* rowbuf = rings + (W + 1) * NC * MSA_RING;      // NC x lds_row_words
+  unsigned* codes = reinterpret_cast<unsigned*>(rowbuf + NC * kp.lds_row_words);  // 4 copies
+  const int code_dwords = kp.lds_code_bytes / 4;
+
+  for (;;) {
+    // ---- ticket ----
+    if (threadIdx.x == 0) misc[0] = atomicAdd(a.ticket, 1);
+    __syncthreads();
+    const int item = misc[0];
+    __syncthreads();
+    if (item >= kp.n_items) break;
+
+    int pair, k0, ns, group;
+    if (kp.single) {
+      pair = 0;
+      group = item;
+      k0 = item * W;
+      const msa_pair_desc pd0 = a.pairs[0];
+      const int S = (pd0.m + 63) / 64;
+      ns = min(W, S - k0);
+    } else {
+      pair = item;
+      group = 0;
+      k0 = 0;
+      ns = (a.pairs[item].m + 63) / 64;
+    }
+    const msa_pair_desc pd = a.pairs[pair];
+    const int m = pd.m, n = pd.n;
+    const int S_pair = (m + 63) / 64;
+
+    // ---- schedule (one lane) ----
+    if (threadIdx.x == 0) {
+      int total = 0;
+      int cmin = 1 << 30, cmax = -(1 << 30);
+      StripeGeom prev;
+      for (int k = 0; k < ns; ++k) {
+        StripeGeom g;
+        stripe_geom(k0 + k, m, n, kp.band, g);
+        int T = 0;
+        if (k > 0) {
+          const int D = (g.cs - prev.cs + 78) / MSA_K + 1;  // cs diff >= -15 -> numerator > 0
+          T = prev.T + D;
+          if (k >= W) {
+            const StripeGeom& o = sched[k - W];
+            T = max(T, o.T + o.P);
+          }
+        }
+        g.T = T;
+        sched[k] = g;
+        prev = g;
+        total = max(total, T + g.P);
+        cmin = min(cmin, g.cs - 64);
+        cmax = max(cmax, g.cs + g.P * MSA_K);
+      }
+      misc[1] = total;
+      misc[2] = cmin & ~3;  // code window base column (multiple of 4)
+      misc[3] = cmax;
+    }
+    __syncthreads();
+    const int total = misc[1];
+    const int cbase = misc[2];
+    const int cwin = misc[3] - cbase + 8;  // bytes needed per copy
+
+    // ---- column codes -> 4 byte-shifted LDS copies ----
+    {
+      const uint8_t* Bp = a.B + pd.b_off;
+      const int nd = min((cwin + 3) / 4, code_dwords);
+      for (int idx = threadIdx.x; idx < 4 * nd; idx += blockDim.x) {
+        const int cp = idx / nd, d = idx - cp * nd;
+        unsigned word = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int col = cbase + 4 * d + cp + b;
+          const unsigned code = (col >= 1 && col <= n) ? (unsigned)Bp[col - 1] : 0u;
+          word |= (code & 7u) << (8 * b);
+        }
+        codes[cp * code_dwords + d] = word;
+      }
+    }
+    __syncthreads();
+
+    // ---- per-wave stripe loop over global phases ----
+    LaneState<ALG> L;
+    int cur = w;
+    StripeGeom sg;
+    int src = SRC_BORDER, snk = SNK_NONE;
+    int in_base = 0;  // ring/row index base for inputs (relative to this stripe's cs)
+    int out_cs = 0;   // consumer cs (for output indexing)
+    int out_chi = 0;  // producer c_hi seen by the consumer (input masking)
+    int* ring_in = nullptr;
+    int* ring_out = nullptr;
+    const int* in_ptr = nullptr;  // LDS input rows: in_ptr + v*in_vs + ((16q + 4u) & in_mask)
+    int in_vs = MSA_RING, in_mask = MSA_RING - 1;
+    int* out_ptr = nullptr;       // LDS output rows: out_ptr + v*out_vs + ((x + out_add) & out_mask)
+    int out_vs = MSA_RING, out_mask = MSA_RING - 1, out_add = 0, out_lim = 1 << 30;
+    unsigned long long* g_in = nullptr;
+    unsigned long long* g_out = nullptr;
+    size_t obase = 0;  // element (O_H/O_TAB) or byte (O_DIR) base of this stripe in the output
+    // prefetched granules (SRC_GLOBAL), A = 3 phases ahead, lanes 0..15
+    unsigned long long G0[NC], G1[NC], G2[NC];
+    const unsigned ep = kp.epoch;
+
+    for (int ph = 0; ph < total; ++ph) {
+      if (cur < ns) {
+        const int Tc = sched[cur].T;
+        if (ph == Tc) {
+          // ---- stripe init ----
+          sg = sched[cur];
+          const int ks = k0 + cur;  // pair-local stripe index
+          L.i = 64 * ks + lane + 1;
+          const int ivalid = min(L.i, m);
+          L.tmin = jlo_of(L.i, kp.band) - sg.cs + lane;
+          L.tmax = (L.i <= m) ? jhi_of(L.i, n, kp.band) - sg.cs + lane : -1;
+          int lb[3];
+          border_left<ALG>(kp, ivalid, lb);
+          if (kp.band >= 0 && jlo_of(L.i, kp.band) > 1) lb[0] = lb[1] = lb[2] = MSA_NEG;
+#pragma unroll
+          for (int v = 0; v < 3; ++v) { L.LB[v] = lb[v]; L.S[v] = lb[v]; L.U[v] = MSA_NEG; L.fin[v] = 0; }
+          L.best = 0;
+          L.bt = -1;
+          // substitution profile of this row (codes 0..7)
+          {
+            const unsigned ac = (L.i <= m) ? (a.A[pd.a_off + L.i - 1] & 7u) : 0u;
+            int sm, sx;
+            if constexpr (ALG == MSA_ALG_REF || ALG == MSA_ALG_NWA) { sm = 1; sx = 0; }
+            else if constexpr (ALG == MSA_ALG_PART) { sm = 0; sx = 1; }
+            else { sm = kp.match; sx = kp.mismatch; }
+            const unsigned bx = (unsigned)(sx & 0xff) * 0x01010101u;
+            unsigned lo = bx, hi = bx;
+            const unsigned bm = (unsigned)(sm & 0xff);
+            if (ac < 4) lo = (lo & ~(0xffu << (8 * ac))) | (bm << (8 * ac));
+            else hi = (hi & ~(0xffu << (8 * (ac - 4)))) | (bm << (8 * (ac - 4)));
+            L.plo = lo;
+            L.phi = hi;
+          }
+          // code stream: lane reads bytes starting at column cs - lane
+          {
+            const int b0 = sg.cs - lane - cbase;  // >= 1 by construction
+            L.cw_copy = b0 & 3;
+            L.cw_base = L.cw_copy * code_dwords + (b0 >> 2);
+          }
+          // input source / output sink
+          if (cur == 0) {
+            if (kp.single && group > 0) src = SRC_GLOBAL; else src = SRC_BORDER;
+          } else {
+            src = (cur % W == 0) ? SRC_ROW : SRC_RING;
+          }
+          if (cur == ns - 1) {
+            snk = (kp.single && ks < S_pair - 1) ? SNK_GLOBAL : SNK_NONE;
+          } else {
+            snk = (cur % W == W - 1) ? SNK_ROW : SNK_RING;
+          }
+          ring_in = rings + ((w + W - 1) % W) * NC * MSA_RING;
+          ring_out = rings + w * NC * MSA_RING;
+          if (src == SRC_GLOBAL) ring_in = rings + W * NC * MSA_RING;
+          if (src == SRC_ROW) {
+            in_ptr = rowbuf + MSA_ROWOFF;
+            in_vs = kp.lds_row_words;
+            in_mask = 0x3fffffff;
+          } else {
+            in_ptr = ring_in;
+            in_vs = MSA_RING;
+            in_mask = MSA_RING - 1;
+          }
+          if (snk == SNK_ROW) {
+            out_ptr = rowbuf;
+            out_vs = kp.lds_row_words;
+            out_mask = 0x3fffffff;
+            out_add = MSA_ROWOFF;
+            out_lim = kp.lds_row_words - 4;
+          } else {
+            out_ptr = ring_out;
+            out_vs = MSA_RING;
+            out_mask = MSA_RING - 1;
+            out_add = 0;
+            out_lim = 1 << 30;
+          }
+          if (snk != SNK_NONE) {
+            StripeGeom gn;
+            stripe_geom(ks + 1, m, n, kp.band, gn);
+            out_cs = gn.cs;
+          }
+          {
+            // c_hi of the producer row above (input masking, banded)
+            if (ks > 0) {
+              StripeGeom gp;
+              stripe_geom(ks - 1, m, n, kp.band, gp);
+              out_chi = gp.c_hi;
+            } else {
+              out_chi = n;
+            }
+          }
+          g_in = (src == SRC_GLOBAL) ? a.gbuf + (size_t)(group - 1) * NC * a.gbuf_stride : nullptr;
+          g_out = (snk == SNK_GLOBAL) ? a.gbuf + (size_t)group * NC * a.gbuf_stride : nullptr;
+          if constexpr (OUT == MSA_OUT_DIR) obase = (size_t)pd.out_off + (size_t)ks * pd.pmax * MSA_K * 64;
+          else obase = (size_t)pd.out_off + (size_t)ks * pd.pmax * MSA_K * 64;
+          in_base = 0;
+          if (src == SRC_GLOBAL) {
+            // prefetch phases 0,1,2 (synchronous start)
+#pragma unroll
+            for (int v = 0; v < NC; ++v) {
+              const int c0 = sg.cs + (lane & 15);
+              G0[v] = gload(g_in + (size_t)v * a.gbuf_stride + min(c0, a.gbuf_stride - 1 - MSA_GOFF) + MSA_GOFF);
+              G1[v] = gload(g_in + (size_t)v * a.gbuf_stride + min(c0 + 16, a.gbuf_stride - 1 - MSA_GOFF) + MSA_GOFF);
+              G2[v] = gload(g_in + (size_t)v * a.gbuf_stride + min(c0 + 32, a.gbuf_stride - 1 - MSA_GOFF) + MSA_GOFF);
+            }
+          }
+        }
+        if (ph >= Tc) {
+          const int q = ph - Tc;
+          // ---- global input: verify + stage phase q into ring_in ----
+          if (src == SRC_GLOBAL) {
+            const int col = sg.cs + 16 * q + (lane & 15);
+            const bool need = (lane < 16) && (col <= out_chi) && (col <= n);
+#pragma unroll
+            for (int v = 0; v < NC; ++v) {
+              unsigned long long gv = G0[v];
+              // wave-uniform spin: every lane re-polls until all needed tags match
+              bool ok = !need || ((unsigned)(gv >> 32) == ep);
+              unsigned spins = 0;
+              while (!__all(ok)) {
+                __builtin_amdgcn_s_sleep(1);
+                const unsigned long long r = gload(g_in + (size_t)v * a.gbuf_stride + col + MSA_GOFF);
+                gv = ok ? gv : r;
+                ok = !need || ((unsigned)(gv >> 32) == ep);
+                if (++spins > (1u << 24)) {
+                  if (lane == 0) atomicExch(a.err, 1);
+                  break;
+                }
+              }
+              if (lane < 16) ring_in[v * MSA_RING + ((16 * q + lane) & (MSA_RING - 1))] = (int)(unsigned)gv;
+              asm volatile("" ::: "memory");  // keep the staging write ahead of the int4 reads below
+              G0[v] = G1[v];
+              G1[v] = G2[v];
+              // unconditional prefetch (address clamped into the buffer) so no wait is forced here
+              const int cpre = min(sg.cs + 16 * (q + 3) + (lane & 15), a.gbuf_stride - 1 - MSA_GOFF);
+              G2[v] = gload(g_in + (size_t)v * a.gbuf_stride + cpre + MSA_GOFF);
+            }
+          }
+          const bool masked = (16 * q < sg.mask_lo) || (16 * q + 15 > sg.mask_hi);
+          const bool inmask = (sg.cs + 16 * q + 15 > out_chi);
+          // code words for this phase: 16 bytes = 4 dwords
+          unsigned cw[4];
+          {
+            const unsigned* cp = codes + L.cw_base + 4 * q;
+            cw[0] = cp[0]; cw[1] = cp[1]; cw[2] = cp[2]; cw[3] = cp[3];
+          }
+          unsigned dirw[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            // inputs for 4 steps
+            int IN[NC][4];
+            if (src == SRC_BORDER) {
+#pragma unroll
+              for (int kk = 0; kk < 4; ++kk) {
+                int bv[3];
+                border_top<ALG>(kp, sg.cs + 16 * q + 4 * u + kk, bv);
+#pragma unroll
+                for (int v = 0; v < NC; ++v) IN[v][kk] = bv[v];
+              }
+            } else {
+              const int* base = in_ptr + ((16 * q + 4 * u) & in_mask);
+#pragma unroll
+              for (int v = 0; v < NC; ++v) {
+                const int4 x = *reinterpret_cast<const int4*>(base + v * in_vs);
+                IN[v][0] = x.x; IN[v][1] = x.y; IN[v][2] = x.z; IN[v][3] = x.w;
+              }
+              if (inmask) {
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                  const bool o = sg.cs + 16 * q + 4 * u + kk > out_chi;
+#pragma unroll
+                  for (int v = 0; v < NC; ++v) IN[v][kk] = o ? MSA_NEG : IN[v][kk];
+                }
+              }
+            }
+            const unsigned s4 = __builtin_amdgcn_perm(L.phi, L.plo, cw[u]);
+            int hist[NC][4];
+            unsigned dq = 0;
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+              const int t = 16 * q + 4 * u + kk;
+              const int s = ((int)(s4 << (24 - 8 * kk))) >> 24;
+              int inv[3];
+#pragma unroll
+              for (int v = 0; v < NC; ++v) inv[v] = IN[v][kk];
+              int cr[3];
+              unsigned d;
+              if (masked) d = step<ALG, OUT, true, TRACKPOS>(kp, L, inv, s, t, cr);
+              else d = step<ALG, OUT, false, TRACKPOS>(kp, L, inv, s, t, cr);
+#pragma unroll
+              for (int v = 0; v < NC; ++v) hist[v][kk] = cr[v];
+              dq |= d << (8 * kk);
+            }
+            dirw[u] = dq;
+            // cell outputs
+            const size_t qi = (size_t)(4 * q + u) * 64 + lane;  // int4 index within stripe block
+            if constexpr (OUT == MSA_OUT_H) {
+              int4 hv;
+              if constexpr (ALG == MSA_ALG_REF || ALG == MSA_ALG_PART) {
+                hv = make_int4(imax3(hist[0][0], hist[1][0], hist[2][0]), imax3(hist[0][1], hist[1][1], hist[2][1]),
+                               imax3(hist[0][2], hist[1][2], hist[2][2]), imax3(hist[0][3], hist[1][3], hist[2][3]));
+              } else {
+                hv = make_int4(hist[0][0], hist[0][1], hist[0][2], hist[0][3]);
+              }
+              reinterpret_cast<int4*>(a.outH + obase)[qi] = hv;
+            } else if constexpr (OUT == MSA_OUT_TAB) {
+              reinterpret_cast<int4*>(a.outH + obase)[qi] = make_int4(hist[0][0], hist[0][1], hist[0][2], hist[0][3]);
+              reinterpret_cast<int4*>(a.outT2 + obase)[qi] = make_int4(hist[1][0], hist[1][1], hist[1][2], hist[1][3]);
+              reinterpret_cast<int4*>(a.outT3 + obase)[qi] = make_int4(hist[2][0], hist[2][1], hist[2][2], hist[2][3]);
+            }
+            // hand the bottom row to the next stripe (lane 63)
+            if (snk != SNK_NONE && lane == 63) {
+              const int x = (sg.cs + 16 * q + 4 * u - 63 - out_cs + out_add) & out_mask;  // multiple of 4
+              if (x >= 0 && x <= out_lim) {
+                int* dst = out_ptr + x;
+#pragma unroll
+                for (int v = 0; v < NC; ++v)
+                  *reinterpret_cast<int4*>(dst + v * out_vs) = make_int4(hist[v][0], hist[v][1], hist[v][2], hist[v][3]);
+              }
+            }
+          }
+          if constexpr (OUT == MSA_OUT_DIR) {
+            reinterpret_cast<uint4*>(a.outDir + obase)[(size_t)q * 64 + lane] = make_uint4(dirw[0], dirw[1], dirw[2], dirw[3]);
+          }
+          // global sink: granules for the 16 columns produced this phase
+          if (snk == SNK_GLOBAL) {
+            asm volatile("" ::: "memory");  // lane 63's int4 ring writes stay ahead of these reads
+            if (lane < 16) {
+              const int x = sg.cs + 16 * q - 63 - out_cs + lane;
+              const int col = sg.cs + 16 * q - 63 + lane;
+              if (col + MSA_GOFF >= 0 && col + MSA_GOFF < a.gbuf_stride) {
+#pragma unroll
+                for (int v = 0; v < NC; ++v) {
+                  const int val = ring_out[v * MSA_RING + (x & (MSA_RING - 1))];
+                  gstore(g_out + (size_t)v * a.gbuf_stride + col + MSA_GOFF,
+                         ((unsigned long long)ep << 32) | (unsigned)val);
+                }
+              }
+            }
+          }
+          if (q == sg.P - 1) {
+            // ---- stripe finalize ----
+            const int ks = k0 + cur;
+            msa_stripe_meta* md = a.meta + pd.stripe0 + ks;
+            if constexpr (ALG == MSA_ALG_SWL || ALG == MSA_ALG_SWA) {
+              // first max in row-major order: max best, then min row
+              int b = (L.i <= m) ? L.best : INT32_MIN;
+              int bi = L.i;
+              int bj = sg.cs + L.bt - lane;
+#pragma unroll
+              for (int off = 32; off >= 1; off >>= 1) {
+                const int ob = __shfl_xor(b, off);
+                const int oi = __shfl_xor(bi, off);
+                const int oj = __shfl_xor(bj, off);
+                if (ob > b || (ob == b && oi < bi)) { b = ob; bi = oi; bj = oj; }
+              }
+              if (lane == 0) {
+                md->best = b;
+                md->best_i = bi;
+                md->best_j = TRACKPOS ? bj : -1;
+              }
+            } else {
+              if (L.i == m) {
+                md->fin[0] = L.fin[0];
+                md->fin[1] = L.fin[1];
+                md->fin[2] = L.fin[2];
+                md->has_fin = 1;
+              }
+            }
+            if (lane == 0) {
+              md->cs = sg.cs;
+              md->phases = sg.P;
+            }
+            cur += W;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Per-pair reduction of the stripe results.
+// ---------------------------------------------------------------------------
+struct PairResult {
+  int32_t score, status;
+  int64_t end_i, end_j;
+  int32_t fin[3];
+  int32_t pad;
+};
+
+__global__ void reduce_pairs_kernel(const msa_pair_desc* pairs, const msa_stripe_meta* meta, int n_pairs, int sw,
+                                    PairResult* out) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_pairs) return;
+  const msa_pair_desc pd = pairs[p];
+  const int S = (pd.m + 63) / 64;
+  PairResult r;
+  r.status = 0;
+  r.pad = 0;
+  r.fin[0] = r.fin[1] = r.fin[2] = 0;
+  if (sw) {
+    int b = 0, bi = 0, bj = 0;  // empty alignment: score 0 at (0,0)
+    for (int s = 0; s < S; ++s) {
+      const msa_stripe_meta md = meta[pd.stripe0 + s];
+      if (md.best > b) { b = md.best; bi = md.best_i; bj = md.best_j; }
+    }
+    r.score = b;
+    r.end_i = bi;
+    r.end_j = bj;
+  } else {
+    const msa_stripe_meta md = meta[pd.stripe0 + S - 1];
+    r.fin[0] = md.fin[0];
+    r.fin[1] = md.fin[1];
+    r.fin[2] = md.fin[2];
+    r.score = max(max(md.fin[0], md.fin[1]), md.fin[2]);
+    r.end_i = pd.m;
+    r.end_j = pd.n;
+    r.status = md.has_fin ? 0 : -1;
+  }
+  out[p] = r;
+}
+
+// ---------------------------------------------------------------------------
+// Order-independent digest of an H output in the skewed layout (matches
+// oracle orc_checksum_h): sum mix(i,j) * (uint32)H(i,j) over valid cells.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__global__ void checksum_kernel(const int32_t* H, const msa_pair_desc* pairs, const msa_stripe_meta* meta, int pair,
+                                int band, unsigned long long* out) {
+  const msa_pair_desc pd = pairs[pair];
+  const int S = (pd.m + 63) / 64;
+  const long long per_stripe = (long long)pd.pmax * MSA_K * 64;
+  const long long total = per_stripe * S;
+  unsigned long long acc = 0;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int s = (int)(e / per_stripe);
+    const long long rem = e - (long long)s * per_stripe;
+    const int quad = (int)(rem >> 8);   // /(64*4)
+    const int r = (int)((rem >> 2) & 63);
+    const int t = quad * 4 + (int)(rem & 3);
+    const int i = 64 * s + r + 1;
+    const int j = meta[pd.stripe0 + s].cs + t - r;
+    if (i > pd.m || j < 1 || j > pd.n) continue;
+    if (band >= 0 && (i - j > band || j - i > band)) continue;
+    const unsigned long long mix = splitmix64(((unsigned long long)i << 32) | (unsigned)j) | 1ull;
+    acc += mix * (unsigned long long)(unsigned)H[pd.out_off + e];
+  }
+  // wave reduce
+  for (int off = 32; off >= 1; off >>= 1) {
+    const unsigned lo = __shfl_xor((unsigned)acc, off), hi = __shfl_xor((unsigned)(acc >> 32), off);
+    acc += ((unsigned long long)hi << 32) | lo;
+  }
+  if ((threadIdx.x & 63) == 0) atomicAdd(out, acc);
+}
+
+}  // namespace msa
+
+namespace msa {
+
+// ---------------------------------------------------------------------------
+// findPartitionParallel (partial.cpp:81-146) on device.  For every k in
+// [1,p) it reduces max(T1+R1, T2+R2+h, T3+R3+h) (int32 wrap) over the row band
+// rows [k*bm, (k+1)*bm) (scan order i, then j) and the column band columns
+// [k*bn, (k+1)*bn) (scan order j, then i); the first maximum in scan order
+// wins (the reference's strict '>').  Key = (val ^ 0x80000000) << 32 |
+// (~scan_idx & 0x3fffffff) << 2 | type, reduced with 64-bit atomicMax.
+// Forward planes F* and reverse planes R' (reverse fill = forward fill of the
+// reversed strings) are read in the skewed stripe layout.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int skew_get(const int32_t* plane, const msa_pair_desc& pd, const msa_stripe_meta* meta,
+                                        int i, int j) {
+  const int s = (i - 1) >> 6, r = (i - 1) & 63;
+  const int t = j - meta[pd.stripe0 + s].cs + r;
+  const size_t e = (size_t)pd.out_off + (((size_t)s * pd.pmax * 4 + (t >> 2)) * 64 + r) * 4 + (t & 3);
+  return plane[e];
+}
+
+__global__ void partition_kernel(const int32_t* F1, const int32_t* F2, const int32_t* F3, const int32_t* R1,
+                                 const int32_t* R2, const int32_t* R3, const msa_pair_desc* pdf,
+                                 const msa_pair_desc* pdr, const msa_stripe_meta* mf, const msa_stripe_meta* mr,
+                                 int p, int hh, unsigned long long* keys) {
+  const msa_pair_desc f = pdf[0], rv = pdr[0];
+  const int m = f.m, n = f.n;
+  const int bm = m / p, bn = n / p;
+  const long long rowcells = (long long)bm * n, colcells = (long long)bn * m;
+  const long long total = (long long)(p - 1) * (rowcells + colcells);
+  // thread-local best per slot; flushed when the (monotone) slot changes
+  int cur_slot = -1;
+  unsigned long long cur_key = 0;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    int k, i, j, slot;
+    long long idx;
+    if (e < (long long)(p - 1) * rowcells) {
+      k = 1 + (int)(e / rowcells);
+      idx = e - (long long)(k - 1) * rowcells;
+      i = k * bm + (int)(idx / n);
+      j = 1 + (int)(idx % n);
+      if (i > m) continue;
+      slot = 2 * k;
+    } else {
+      const long long e2 = e - (long long)(p - 1) * rowcells;
+      k = 1 + (int)(e2 / colcells);
+      idx = e2 - (long long)(k - 1) * colcells;
+      j = k * bn + (int)(idx / m);
+      i = 1 + (int)(idx % m);
+      if (j > n) continue;
+      slot = 2 * k + 1;
+    }
+    const int f1 = skew_get(F1, f, mf, i, j), f2 = skew_get(F2, f, mf, i, j), f3 = skew_get(F3, f, mf, i, j);
+    const int ri = m + 1 - i, rj = n + 1 - j;
+    const int r1 = skew_get(R1, rv, mr, ri, rj), r2 = skew_get(R2, rv, mr, ri, rj), r3 = skew_get(R3, rv, mr, ri, rj);
+    const int val = imax3(wrap_add(f1, r1), wrap_add(wrap_add(f2, r2), hh), wrap_add(wrap_add(f3, r3), hh));
+    if (val == INT32_MIN) continue;  // can never beat the reference's INT_MIN start
+    const unsigned type = (unsigned)firstmax3(f1, f2, f3);
+    const unsigned long long key = ((unsigned long long)((unsigned)val ^ 0x80000000u) << 32) |
+                                   ((unsigned long long)((~(unsigned)idx) & 0x3fffffffu) << 2) | type;
+    if (slot != cur_slot) {
+      if (cur_slot >= 0 && cur_key) atomicMax(keys + cur_slot, cur_key);
+      cur_slot = slot;
+      cur_key = 0;
+    }
+    cur_key = key > cur_key ? key : cur_key;
+  }
+  if (cur_slot >= 0 && cur_key) atomicMax(keys + cur_slot, cur_key);
+}
+
+}  // namespace msa

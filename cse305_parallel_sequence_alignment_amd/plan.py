@@ -1,0 +1,166 @@
+"""Device-resident plans over libmsa (torch tensors as device memory/streams).
+
+PyTorch only provides device allocation, streams and ``torch.distributed``
+plumbing here; every DP cell is computed by the HIP stripe kernel.
+
+Skewed stripe layout of per-cell outputs (H / DIR / TAB planes), per pair:
+stripe s (rows 64s+1..64s+64) owns ``pmax*16*64`` elements; element
+``((s*pmax*4 + t//4)*64 + r)*4 + t%4`` (DIR: ``(s*pmax + t//16)*1024 + r*16 + t%16``)
+holds cell ``(i, j) = (64s + r + 1, cs_s + t - r)``, cs_s from the stripe meta.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib as LB
+
+META_FIELDS = 12  # int32 per stripe: cs, phases, best, best_i, best_j, fin0..2, has_fin, pad*3
+
+
+def _stream_ptr(stream):
+    if stream is None:
+        import torch
+
+        return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    if isinstance(stream, int):
+        return C.c_void_p(stream)
+    return C.c_void_p(stream.cuda_stream)
+
+
+def _ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+@dataclass
+class PairGeom:
+    m: int
+    n: int
+    stripe0: int
+    pmax: int
+    out_off: int
+
+
+class Plan:
+    """One launch shape: ``n_pairs`` pairs of (m_k, n_k) codes at (a_off_k, b_off_k)."""
+
+    def __init__(self, alg: int, cells: int, ms, ns, a_offs, b_offs, match=1, mismatch=0, gap_open=1,
+                 gap_extend=1, start_type=-1, band=-1, track_end=False, single=None):
+        L = LB.lib()
+        self.alg, self.cells = alg, cells
+        self.ms = [int(x) for x in ms]
+        self.ns = [int(x) for x in ns]
+        npairs = len(self.ms)
+        if single is None:
+            single = npairs == 1
+        self._arrs = [(C.c_int64 * npairs)(*v) for v in (self.ms, self.ns, [int(x) for x in a_offs],
+                                                         [int(x) for x in b_offs])]
+        d = LB.PlanDesc(alg=alg, cells=cells, match=match, mismatch=mismatch, gap_open=gap_open,
+                        gap_extend=gap_extend, start_type=start_type, band=band, track_end=int(bool(track_end)),
+                        single=int(bool(single)), n_pairs=npairs, m=self._arrs[0], n=self._arrs[1],
+                        a_off=self._arrs[2], b_off=self._arrs[3])
+        self._h = C.c_void_p()
+        LB.check(L.msa_plan_create(C.byref(d), C.byref(self._h)), "msa_plan_create")
+        self.band = band
+        self.single = bool(single)
+        e = C.c_int64()
+        LB.check(L.msa_plan_cells_size(self._h, C.byref(e)), "msa_plan_cells_size")
+        self.cells_elems = e.value
+        self.n_stripes = int(L.msa_plan_stripes(self._h))
+        # host copy of the geometry (same formulas as the C side)
+        self.geom = []
+        s0, off = 0, 0
+        for m, n in zip(self.ms, self.ns):
+            S = (m + 63) // 64
+            pmax = max(stripe_phases(k, m, n, band if alg == LB.NW_BANDED else -1) for k in range(S))
+            self.geom.append(PairGeom(m, n, s0, pmax, off))
+            cells_ = S * pmax * 16 * 64
+            off += (cells_ + 63) & ~63
+            s0 += S
+
+    def __del__(self):
+        try:
+            if self._h:
+                LB.lib().msa_plan_destroy(self._h)
+                self._h = C.c_void_p()
+        except Exception:
+            pass
+
+    def run(self, dA, dB, out0=None, out1=None, out2=None, stream=None):
+        LB.check(LB.lib().msa_plan_run(self._h, _ptr(dA), _ptr(dB), _ptr(out0), _ptr(out1), _ptr(out2),
+                                       _stream_ptr(stream)), "msa_plan_run")
+
+    def results(self, stream=None):
+        n = len(self.ms)
+        arr = (LB.PairResult * n)()
+        LB.check(LB.lib().msa_plan_results(self._h, arr, _stream_ptr(stream)), "msa_plan_results")
+        return [dict(score=r.score, status=r.status, end=(r.end_i, r.end_j), fin=tuple(r.fin)) for r in arr]
+
+    def stripe_meta(self, stream=None) -> np.ndarray:
+        out = np.zeros((self.n_stripes, META_FIELDS), dtype=np.int32)
+        LB.check(LB.lib().msa_plan_stripe_meta(self._h, out.ctypes.data_as(C.c_void_p), self.n_stripes,
+                                               _stream_ptr(stream)), "msa_plan_stripe_meta")
+        return out
+
+    def checksum(self, dH, pair=0, stream=None) -> int:
+        v = C.c_uint64()
+        LB.check(LB.lib().msa_plan_checksum(self._h, _ptr(dH), pair, C.byref(v), _stream_ptr(stream)),
+                 "msa_plan_checksum")
+        return int(v.value)
+
+    def kernel_ms(self) -> float:
+        v = C.c_float()
+        LB.check(LB.lib().msa_plan_last_kernel_ms(self._h, C.byref(v)), "msa_plan_last_kernel_ms")
+        return float(v.value)
+
+    # ---- host-side layout helpers (tests / drop-in API) ----
+    def deskew(self, flat: np.ndarray, pair: int, meta: np.ndarray, fill=0) -> np.ndarray:
+        """Row-major (m+1) x (n+1) matrix of a pair's int32 cells (row/col 0 = fill)."""
+        g = self.geom[pair]
+        S = (g.m + 63) // 64
+        blk = flat[g.out_off:g.out_off + S * g.pmax * 1024].reshape(S, g.pmax * 4, 64, 4)
+        out = np.full((g.m + 1, g.n + 1), fill, dtype=flat.dtype)
+        T = g.pmax * 16
+        t = np.arange(T)
+        r = np.arange(64)
+        for s in range(S):
+            cs = int(meta[g.stripe0 + s, 0])
+            vals = blk[s].transpose(1, 0, 2).reshape(64, T)  # [r][t]
+            i = 64 * s + r + 1
+            j = cs + t[None, :] - r[:, None]
+            ok = (i[:, None] <= g.m) & (j >= 0) & (j <= g.n)
+            ii = np.broadcast_to(i[:, None], j.shape)
+            out[ii[ok], j[ok]] = vals[ok]
+        return out
+
+    def deskew_dir(self, flat: np.ndarray, pair: int, meta: np.ndarray) -> np.ndarray:
+        g = self.geom[pair]
+        S = (g.m + 63) // 64
+        blk = flat[g.out_off:g.out_off + S * g.pmax * 1024].reshape(S, g.pmax, 64, 16)
+        out = np.zeros((g.m + 1, g.n + 1), dtype=np.uint8)
+        T = g.pmax * 16
+        t = np.arange(T)
+        r = np.arange(64)
+        for s in range(S):
+            cs = int(meta[g.stripe0 + s, 0])
+            vals = blk[s].transpose(1, 0, 2).reshape(64, T)
+            i = 64 * s + r + 1
+            j = cs + t[None, :] - r[:, None]
+            ok = (i[:, None] <= g.m) & (j >= 1) & (j <= g.n)
+            ii = np.broadcast_to(i[:, None], j.shape)
+            out[ii[ok], j[ok]] = vals[ok]
+        return out
+
+
+def stripe_phases(k: int, m: int, n: int, band: int) -> int:
+    """Python restatement of stripe_geom().P (msa_kernels.hip) for host layout sizing."""
+    i0 = 64 * k + 1
+    rlast = min(63, m - 64 * k - 1)
+    ilast = i0 + rlast
+    jlo = 1 if band < 0 else max(1, i0 - band)
+    lead = (jlo - 1 - k) % 16 + 1
+    cs = jlo - lead
+    jhi = n if band < 0 else min(n, ilast + band)
+    return (jhi - cs + rlast) // 16 + 1

@@ -1,0 +1,173 @@
+/*
+ * msa.h -- C-ABI of the MI355X-native pairwise-alignment library (libmsa.so).
+ *
+ * Plain pointers and sizes only (no torch / HIP types in the signatures; a
+ * stream is passed as `void*` holding a hipStream_t, NULL = default stream).
+ * Every function returns an msa_status (0 = OK, < 0 = error); nothing throws
+ * across this boundary.  All compute runs in hand-written HIP kernels for
+ * gfx950; there is no CPU fallback: without a usable GPU the calls return
+ * MSA_ERR_NODEV.
+ *
+ * Reference interfaces each entry point replaces (D-2n/CSE305_Parallel_Sequence_Alignment):
+ *   msa_main_alignment   int main_alignment_function(char*,char*,size_t,size_t,size_t,double,double)
+ *                        alignment_algorithm/main_alignment.h:38, .cpp:353-410
+ *                        (with OptimalAlignmentMapThread :11-22 and print_seq :32-55)
+ *   msa_subproblem       class Subproblem ctor + compute_tables() + find_alignment()
+ *                        alignment_algorithm/subproblem_alignment.h:36-74,
+ *                        subproblem_alignment.cpp:329-355 (fill), :105-172 (traceback)
+ *   msa_partial_partition findPartialBalancedPartitionParallel(...)
+ *                        sequence_alignment/partial.h:41, partial.cpp:149-163
+ *   msa_partial_tables   initializeTables/initializeReverseTables/fillTablesParallel/
+ *                        fillReverseTablesParallel, partial.h:25-35, partial.cpp:13-79
+ *   msa_plan_*           device-resident batch / single-pair fills (build extension:
+ *                        configs C2-C5 of BASELINE.json; no reference counterpart,
+ *                        same cell recurrence family as subproblem_alignment.cpp:396-398)
+ */
+#ifndef MSA_H
+#define MSA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status ------------------------------------------------------------ */
+typedef enum msa_status {
+  MSA_OK = 0,
+  MSA_ERR_ARG = -1,          /* bad argument (size 0 where the path needs >0, NULL, ...) */
+  MSA_ERR_ALPHABET = -2,     /* more than 8 distinct symbols in a pair */
+  MSA_ERR_HIP = -3,          /* a HIP runtime call failed */
+  MSA_ERR_NODEV = -4,        /* no gfx950 device visible */
+  MSA_ERR_UNSUPPORTED = -5,  /* e.g. non-integral g/h (the GPU path is exact int32) */
+  MSA_ERR_TIMEOUT = -6,      /* a cross-workgroup wait exceeded its bound */
+  MSA_ERR_NOMEM = -7,
+  MSA_ERR_CAPACITY = -8,     /* caller buffer too small */
+  MSA_ERR_NOMATCH = -9       /* traceback found no predecessor (cannot happen for integral g,h) */
+} msa_status;
+
+const char* msa_status_string(int status);
+int msa_version(void);
+/* number of usable gfx950 devices */
+int msa_device_count(int* count);
+
+/* Node of an alignment path: the reference's `align` struct
+ * (subproblem_alignment.h:8-13) without the `next` pointer. */
+typedef struct msa_node {
+  uint64_t i;
+  uint64_t j;
+  int32_t t;
+  int32_t pad;
+} msa_node;
+
+/* ---- reference-compatible host-pointer entry points ---------------------
+ * Character arrays follow the reference's conventions: A1/B1 are 1-based
+ * (A1[0] never read), compared for equality only. */
+
+/* main_alignment_function: writes the exact stdout text the reference prints
+ * ("bp1".."bp4" then print_seq's two lines) into `text` (NUL-terminated),
+ * *text_len = its length.  *score = max(T1,T2,T3)[m][n] (not exposed by the
+ * reference; returned for convenience).  p only sets the reference's thread
+ * count and is accepted for signature parity. */
+int msa_main_alignment(const char* A1, const char* B1, size_t m, size_t n, size_t p, double g, double h,
+                       char* text, size_t text_cap, size_t* text_len, double* score);
+
+/* Subproblem(A1,B1,m,n,idA,idB,p,start,end,g,h) -> compute_tables(), and when
+ * nodes != NULL, find_alignment().  After the constructor's swap (m > n) the
+ * tables are (m'+1) x (n'+1), m' = min(m,n); T1/T2/T3 (each NULL or
+ * (m'+1)*(n'+1) int32, row-major) receive the tables with INT32_MIN standing
+ * for -infinity.  nodes[0..*n_nodes) = alignment_begin .. alignment_end;
+ * *end_node = alignment_end; *invert = the constructor's swap flag. */
+int msa_subproblem(const char* A1, const char* B1, size_t m, size_t n, size_t idA, size_t idB, int start_type,
+                   int end_type, double g, double h, int32_t* T1, int32_t* T2, int32_t* T3, msa_node* nodes,
+                   size_t nodes_cap, size_t* n_nodes, msa_node* end_node, int* invert);
+
+/* findPartialBalancedPartitionParallel (partial.cpp:149-163), int32 wrap
+ * semantics; A0/B0 are 0-based (partial.cpp reads A[i-1]).  out receives the
+ * p+1 sorted partition points. */
+int msa_partial_partition(const char* A0, const char* B0, size_t m, size_t n, size_t p, double g, double h,
+                          int start_type, int end_type, msa_node* out, size_t cap, size_t* n_out);
+
+/* The six int32 tables partial.cpp builds: T* (m+1)x(n+1), R* (m+2)x(n+2),
+ * row-major; any pointer may be NULL. */
+int msa_partial_tables(const char* A0, const char* B0, size_t m, size_t n, double g, double h, int start_type,
+                       int end_type, int32_t* T1, int32_t* T2, int32_t* T3, int32_t* R1, int32_t* R2, int32_t* R3);
+
+/* ---- device-resident plans (configs C2-C5) --------------------------------
+ * A plan owns the device scratch for one shape of work; running it launches
+ * the stripe kernel + a tiny per-pair reduction on `stream` (no allocation,
+ * no host sync inside msa_plan_run).  Inputs are uint8 codes in [0,8) already
+ * in device memory (see msa_encode_pair for the host-side code map). */
+typedef enum msa_alg_e {
+  MSA_SW_LINEAR = 0,  /* Smith-Waterman, linear gap (gap_open == gap_extend used) */
+  MSA_SW_AFFINE = 1,  /* Smith-Waterman, affine gap */
+  MSA_NW_BANDED = 2,  /* reference Gotoh (g=gap_extend, h=gap_open-gap_extend), start type -1, optional band */
+  MSA_REF_GOTOH = 3,  /* reference Gotoh T1/T2/T3, any start type, exact -inf */
+  MSA_PARTIAL = 4     /* partial.cpp forward Gotoh, int32 wrap */
+} msa_alg_e;
+
+typedef enum msa_out_e { MSA_CELLS_NONE = 0, MSA_CELLS_H = 1, MSA_CELLS_DIR = 2, MSA_CELLS_TAB = 3 } msa_out_e;
+
+typedef struct msa_plan_desc {
+  int32_t alg;         /* msa_alg_e */
+  int32_t cells;       /* msa_out_e */
+  int32_t match, mismatch;
+  int32_t gap_open;    /* SW: cost of the first gap char; Gotoh: g + h */
+  int32_t gap_extend;  /* SW: each further gap char; Gotoh: g */
+  int32_t start_type;  /* MSA_REF_GOTOH / MSA_PARTIAL */
+  int32_t band;        /* MSA_NW_BANDED: |i-j| <= band, -1 = none */
+  int32_t track_end;   /* SW: also report the end cell (first max, row-major) */
+  int32_t single;      /* 1: one pair spread over many workgroups; 0: one workgroup per pair */
+  int64_t n_pairs;
+  const int64_t* m;    /* host arrays, n_pairs each */
+  const int64_t* n;
+  const int64_t* a_off; /* offsets of each pair's row / column codes in the device arrays */
+  const int64_t* b_off;
+} msa_plan_desc;
+
+typedef struct msa_pair_result {
+  int32_t score;
+  int32_t status;
+  int64_t end_i, end_j;  /* SW: end cell; Gotoh: (m, n) */
+  int32_t fin[3];        /* Gotoh: state at (m, n) (T1,T2,T3 / H,E,F) */
+  int32_t pad;
+} msa_pair_result;
+
+typedef struct msa_plan msa_plan;
+
+int msa_plan_create(const msa_plan_desc* desc, msa_plan** plan);
+void msa_plan_destroy(msa_plan* plan);
+/* Elements (int32 for H/TAB planes, bytes for DIR) the per-cell output needs. */
+int msa_plan_cells_size(const msa_plan* plan, int64_t* elems);
+/* Launch on `stream`.  dA/dB: device code arrays.  cells0..2: device output
+ * (H: cells0; DIR: cells0 as uint8; TAB: three planes), may be NULL for NONE. */
+int msa_plan_run(msa_plan* plan, const uint8_t* dA, const uint8_t* dB, void* cells0, void* cells1, void* cells2,
+                 void* stream);
+/* Copy per-pair results to the host (synchronizes `stream`). */
+int msa_plan_results(msa_plan* plan, msa_pair_result* out, void* stream);
+/* Per-stripe metadata (cs, phases ...) of the last run: 12 int32 per stripe. */
+int msa_plan_stripe_meta(msa_plan* plan, int32_t* out, int64_t cap_stripes, void* stream);
+int64_t msa_plan_stripes(const msa_plan* plan);
+/* Order-independent digest of pair `pair`'s H cells (oracle orc_checksum_h). */
+int msa_plan_checksum(msa_plan* plan, const int32_t* dH, int64_t pair, uint64_t* digest, void* stream);
+/* Device time (ms) of the last msa_plan_run's stripe kernel, from HIP events
+ * recorded on the run's stream (synchronizes). */
+int msa_plan_last_kernel_ms(msa_plan* plan, float* ms);
+
+/* Map the symbols of a pair to codes 0..7 (equality preserved, first-seen
+ * order).  Returns MSA_ERR_ALPHABET for more than 8 distinct symbols. */
+int msa_encode_pair(const char* A0, size_t m, const char* B0, size_t n, uint8_t* codesA, uint8_t* codesB);
+
+/* Host-pointer Smith-Waterman (build extension): score, end cell (first max
+ * in row-major order) and, when cigar != NULL, the traceback as a run-length
+ * M/I/D string (I consumes A, D consumes B) with its start cell. */
+int msa_sw_align(const char* A0, size_t m, const char* B0, size_t n, int32_t match, int32_t mismatch,
+                 int32_t gap_open, int32_t gap_extend, int32_t* score, int64_t* end_i, int64_t* end_j,
+                 int64_t* beg_i, int64_t* beg_j, char* cigar, size_t cigar_cap);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MSA_H */
