@@ -260,7 +260,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   } else {
     kp.n_items = (int)desc->n_pairs;
   }
-  const size_t lds_ints = 16 + (size_t)kp.sched_cap * 8 + (size_t)(MSA_WAVES + 1) * P->nc * MSA_RING +
+  const size_t lds_ints = 16 + (size_t)kp.sched_cap * 8 + (size_t)(2 * MSA_WAVES + 1) * P->nc * MSA_RING +
                           (size_t)P->nc * kp.lds_row_words + (size_t)kp.lds_code_bytes;  // 4 copies = bytes*4/4
   P->lds_bytes = lds_ints * 4;
   if (P->lds_bytes > 160 * 1024) {
@@ -274,7 +274,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     return MSA_ERR_HIP;
   }
   int occ = 1;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)P->fn, 512, P->lds_bytes) != hipSuccess || occ < 1)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)P->fn, MSA_THREADS, P->lds_bytes) != hipSuccess || occ < 1)
     occ = 1;
   hipDeviceProp_t prop;
   int dev = 0;
@@ -351,7 +351,7 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
   a.outT3 = (int32_t*)c2;
   HIPCHK(hipMemsetAsync(P->d_ticket, 0, 64, st));
   HIPCHK(hipEventRecord(P->ev0, st));
-  hipLaunchKernelGGL(P->fn, dim3(P->grid), dim3(512), P->lds_bytes, st, a);
+  hipLaunchKernelGGL(P->fn, dim3(P->grid), dim3(MSA_THREADS), P->lds_bytes, st, a);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(P->ev1, st));
   const int sw = (P->kp.alg == MSA_ALG_SWL || P->kp.alg == MSA_ALG_SWA) ? 1 : 0;

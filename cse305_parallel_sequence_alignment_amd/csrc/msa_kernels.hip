@@ -35,11 +35,14 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "msa_types.h"
 
 #define MSA_WAVES 8
 #define MSA_K 16
-#define MSA_RING 512
+#define MSA_RING 256
+#define MSA_THREADS ((MSA_WAVES + 1) * 64)
 #define MSA_ROWOFF 128
 #define MSA_GOFF 128
 #define MSA_NEG (-(1 << 30))
@@ -63,6 +66,10 @@ __device__ __forceinline__ int imax3(int a, int b, int c) { return imax(imax(a, 
 __device__ __forceinline__ int firstmax3(int a, int b, int c) {
   return (a >= b && a >= c) ? 1 : (b >= c ? 2 : 3);
 }
+// Wave-uniform value into an SGPR: keeps phase-level branches scalar (values
+// read from LDS are otherwise treated as divergent, and every DP step ends up
+// wrapped in exec-mask branching).
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ int wrap_add(int a, int b) { return (int)((unsigned)a + (unsigned)b); }
 __device__ __forceinline__ int wrap_sub(int a, int b) { return (int)((unsigned)a - (unsigned)b); }
 
@@ -315,21 +322,63 @@ __device__ __forceinline__ void gstore(unsigned long long* p, unsigned long long
 enum Src { SRC_BORDER = 0, SRC_RING = 1, SRC_ROW = 2, SRC_GLOBAL = 3 };
 enum Snk { SNK_NONE = 0, SNK_RING = 1, SNK_ROW = 2, SNK_GLOBAL = 3 };
 
+// Loader wave (wave MSA_WAVES): in single mode it pulls the row above the
+// item's first stripe from the previous workgroup's granules (HBM, `sc1`)
+// into the LDS staging ring MSA_LOAD_AHEAD phases ahead, so no compute wave
+// ever waits on a global load.  Prefetch slots are compile-time indices
+// (loop unrolled by MSA_LOAD_AHEAD): no register rotation, hence no forced
+// vmcnt(0) right after a load.
+#define MSA_LOAD_AHEAD 4
+
+template <int NC>
+__device__ __forceinline__ void loader_commit(const KArgs& a, const StripeGeom& s0, int q, unsigned long long gv,
+                                              const unsigned long long* g_in, int* stage, int chi, int n,
+                                              unsigned ep, int lane) {
+  const int v = lane >> 4, l = lane & 15;
+  const int col = s0.cs + 16 * q + l;
+  const bool need = (v < NC) && (col <= chi) && (col <= n) && (q < s0.P);
+  bool ok = !need || ((unsigned)(gv >> 32) == ep);
+  unsigned spins = 0;
+  while (!__all(ok)) {
+    __builtin_amdgcn_s_sleep(1);
+    const int cc = min(col, a.gbuf_stride - 1 - MSA_GOFF);
+    const unsigned long long r = gload(g_in + (size_t)min(v, NC - 1) * a.gbuf_stride + cc + MSA_GOFF);
+    gv = ok ? gv : r;
+    ok = !need || ((unsigned)(gv >> 32) == ep);
+    if (++spins > (1u << 24)) {
+      if (lane == 0) atomicExch(a.err, 1);
+      break;
+    }
+  }
+  if (v < NC) stage[v * MSA_RING + ((16 * q + l) & (MSA_RING - 1))] = (int)(unsigned)gv;
+}
+
+template <int NC>
+__device__ __forceinline__ unsigned long long loader_issue(const KArgs& a, const StripeGeom& s0, int q,
+                                                           const unsigned long long* g_in, int lane) {
+  const int v = min(lane >> 4, NC - 1), l = lane & 15;
+  const int col = min(s0.cs + 16 * q + l, a.gbuf_stride - 1 - MSA_GOFF);
+  return gload(g_in + (size_t)v * a.gbuf_stride + col + MSA_GOFF);
+}
+
 template <int ALG, int OUT, bool TRACKPOS>
-__global__ __launch_bounds__(512) void stripe_kernel(KArgs a) {
+__global__ __launch_bounds__(MSA_THREADS) void stripe_kernel(KArgs a) {
   constexpr int NC = Tr<ALG>::NC;
   constexpr int W = MSA_WAVES;
+  constexpr int LA = MSA_LOAD_AHEAD;
   extern __shared__ __attribute__((aligned(16))) int smem[];
   const msa_kparams& kp = a.kp;
   const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
+  const int w = uni(threadIdx.x >> 6);
 
   // ---- LDS carve (int32 units, all offsets multiples of 4) ----
-  int* misc = smem;                                   // 16 ints
+  int* misc = smem;  // 16 ints
   StripeGeom* sched = reinterpret_cast<StripeGeom*>(smem + 16);
   const int sched_cap = kp.sched_cap;
-  int* rings = smem + 16 + sched_cap * 8;             // (W+1) x NC x RING
-  int* rowbuf = rings + (W + 1) * NC * MSA_RING;      // NC x lds_row_words
+  // rings: [parity 2][wave W][NC][RING] + staging [NC][RING]
+  int* rings = smem + 16 + sched_cap * 8;
+  int* stage = rings + 2 * W * NC * MSA_RING;
+  int* rowbuf = stage + NC * MSA_RING;  // NC x lds_row_words (batch wrap link)
   unsigned* codes = reinterpret_cast<unsigned*>(rowbuf + NC * kp.lds_row_words);  // 4 copies
   const int code_dwords = kp.lds_code_bytes / 4;
 
@@ -337,7 +386,7 @@ __global__ __launch_bounds__(512) void stripe_kernel(KArgs a) {
     // ---- ticket ----
     if (threadIdx.x == 0) misc[0] = atomicAdd(a.ticket, 1);
     __syncthreads();
-    const int item = misc[0];
+    const int item = uni(misc[0]);
     __syncthreads();
     if (item >= kp.n_items) break;
 
@@ -388,9 +437,9 @@ __global__ __launch_bounds__(512) void stripe_kernel(KArgs a) {
       misc[3] = cmax;
     }
     __syncthreads();
-    const int total = misc[1];
-    const int cbase = misc[2];
-    const int cwin = misc[3] - cbase + 8;  // bytes needed per copy
+    const int total = uni(misc[1]);
+    const int cbase = uni(misc[2]);
+    const int cwin = uni(misc[3]) - cbase + 8;  // bytes needed per copy
 
     // ---- column codes -> 4 byte-shifted LDS copies ----
     {
@@ -409,34 +458,93 @@ __global__ __launch_bounds__(512) void stripe_kernel(KArgs a) {
       }
     }
     __syncthreads();
+    const unsigned ep = kp.epoch;
 
-    // ---- per-wave stripe loop over global phases ----
+    if (w == W) {
+      // =================== loader wave ===================
+      const bool act = kp.single && group > 0;
+      StripeGeom s0 = sched[0];
+      s0.cs = uni(s0.cs);
+      s0.P = uni(s0.P);
+      int chi = n;
+      if (k0 > 0) {
+        StripeGeom gp;
+        stripe_geom(k0 - 1, m, n, kp.band, gp);
+        chi = gp.c_hi;
+      }
+      const unsigned long long* g_in = act ? a.gbuf + (size_t)(group - 1) * NC * a.gbuf_stride : a.gbuf;
+      const bool border = (k0 == 0);  // the item holds the pair's first stripe: stage the DP's row 0
+      auto commit_border = [&](int q) {
+        const int v = lane >> 4, l = lane & 15;
+        int bv[3];
+        border_top<ALG>(kp, s0.cs + 16 * q + l, bv);
+        const int val = (v == 0) ? bv[0] : (v == 1 ? bv[1] : bv[2]);
+        if (v < NC) stage[v * MSA_RING + ((16 * q + l) & (MSA_RING - 1))] = val;
+      };
+      if (border) commit_border(0);
+      unsigned long long G[LA];
+      if (act) {
+        // start only once the producer is LA+2 phases ahead, so that every
+        // prefetch below reads an already-published granule (no re-poll stalls)
+        {
+          const int qw = min(s0.P - 1, LA + 1);
+          const int colw = min(min(s0.cs + 16 * qw + 15, chi), n);
+          unsigned spins = 0;
+          while ((unsigned)(gload(g_in + colw + MSA_GOFF) >> 32) != ep) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > (1u << 24)) {
+              if (lane == 0) atomicExch(a.err, 1);
+              break;
+            }
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < LA; ++s) G[s] = loader_issue<NC>(a, s0, s, g_in, lane);
+        loader_commit<NC>(a, s0, 0, G[0], g_in, stage, chi, n, ep, lane);
+      }
+      __syncthreads();  // phase 0 staged before any compute wave reads it
+      for (int ph = 0; ph < total; ph += LA) {
+#pragma unroll
+        for (int s = 0; s < LA; ++s) {
+          const int p = ph + s;
+          if (p < total) {
+            if (act) {
+              if (p + 1 < s0.P) loader_commit<NC>(a, s0, p + 1, G[(s + 1) % LA], g_in, stage, chi, n, ep, lane);
+              if (p + LA < s0.P) G[s] = loader_issue<NC>(a, s0, p + LA, g_in, lane);
+            } else if (border) {
+              if (p + 1 < s0.P) commit_border(p + 1);
+            }
+            __syncthreads();
+          }
+        }
+      }
+      continue;
+    }
+
+    // =================== compute waves ===================
     LaneState<ALG> L;
     int cur = w;
     StripeGeom sg;
-    int src = SRC_BORDER, snk = SNK_NONE;
-    int in_base = 0;  // ring/row index base for inputs (relative to this stripe's cs)
+    int snk = SNK_NONE;
     int out_cs = 0;   // consumer cs (for output indexing)
     int out_chi = 0;  // producer c_hi seen by the consumer (input masking)
-    int* ring_in = nullptr;
     int* ring_out = nullptr;
     const int* in_ptr = nullptr;  // LDS input rows: in_ptr + v*in_vs + ((16q + 4u) & in_mask)
     int in_vs = MSA_RING, in_mask = MSA_RING - 1;
     int* out_ptr = nullptr;       // LDS output rows: out_ptr + v*out_vs + ((x + out_add) & out_mask)
     int out_vs = MSA_RING, out_mask = MSA_RING - 1, out_add = 0, out_lim = 1 << 30;
-    unsigned long long* g_in = nullptr;
     unsigned long long* g_out = nullptr;
     size_t obase = 0;  // element (O_H/O_TAB) or byte (O_DIR) base of this stripe in the output
-    // prefetched granules (SRC_GLOBAL), A = 3 phases ahead, lanes 0..15
-    unsigned long long G0[NC], G1[NC], G2[NC];
-    const unsigned ep = kp.epoch;
+    __syncthreads();  // pairs with the loader's post-staging barrier
 
     for (int ph = 0; ph < total; ++ph) {
       if (cur < ns) {
-        const int Tc = sched[cur].T;
+        const int Tc = uni(sched[cur].T);
         if (ph == Tc) {
           // ---- stripe init ----
           sg = sched[cur];
+          sg.T = uni(sg.T); sg.P = uni(sg.P); sg.cs = uni(sg.cs); sg.lead = uni(sg.lead);
+          sg.mask_lo = uni(sg.mask_lo); sg.mask_hi = uni(sg.mask_hi); sg.c_hi = uni(sg.c_hi);
           const int ks = k0 + cur;  // pair-local stripe index
           L.i = 64 * ks + lane + 1;
           const int ivalid = min(L.i, m);
@@ -470,205 +578,156 @@ __global__ __launch_bounds__(512) void stripe_kernel(KArgs a) {
             L.cw_copy = b0 & 3;
             L.cw_base = L.cw_copy * code_dwords + (b0 >> 2);
           }
-          // input source / output sink
+          // input source: border row, ring of the previous wave (same round
+          // parity), the wrap row buffer, or the loader's staging ring
+          const int par_in = ((cur - 1) / W) & 1;  // round parity of the producer stripe
           if (cur == 0) {
-            if (kp.single && group > 0) src = SRC_GLOBAL; else src = SRC_BORDER;
+            in_ptr = stage; in_vs = MSA_RING; in_mask = MSA_RING - 1;  // loader: row 0 or the previous group
+          } else if (cur % W == 0) {
+            in_ptr = rowbuf + MSA_ROWOFF; in_vs = kp.lds_row_words; in_mask = 0x3fffffff;
           } else {
-            src = (cur % W == 0) ? SRC_ROW : SRC_RING;
+            in_ptr = rings + ((par_in * W + (w - 1)) * NC) * MSA_RING; in_vs = MSA_RING; in_mask = MSA_RING - 1;
           }
           if (cur == ns - 1) {
             snk = (kp.single && ks < S_pair - 1) ? SNK_GLOBAL : SNK_NONE;
           } else {
             snk = (cur % W == W - 1) ? SNK_ROW : SNK_RING;
           }
-          ring_in = rings + ((w + W - 1) % W) * NC * MSA_RING;
-          ring_out = rings + w * NC * MSA_RING;
-          if (src == SRC_GLOBAL) ring_in = rings + W * NC * MSA_RING;
-          if (src == SRC_ROW) {
-            in_ptr = rowbuf + MSA_ROWOFF;
-            in_vs = kp.lds_row_words;
-            in_mask = 0x3fffffff;
-          } else {
-            in_ptr = ring_in;
-            in_vs = MSA_RING;
-            in_mask = MSA_RING - 1;
-          }
+          ring_out = rings + (((cur / W) & 1) * W + w) * NC * MSA_RING;
           if (snk == SNK_ROW) {
-            out_ptr = rowbuf;
-            out_vs = kp.lds_row_words;
-            out_mask = 0x3fffffff;
-            out_add = MSA_ROWOFF;
+            out_ptr = rowbuf; out_vs = kp.lds_row_words; out_mask = 0x3fffffff; out_add = MSA_ROWOFF;
             out_lim = kp.lds_row_words - 4;
           } else {
-            out_ptr = ring_out;
-            out_vs = MSA_RING;
-            out_mask = MSA_RING - 1;
-            out_add = 0;
-            out_lim = 1 << 30;
+            out_ptr = ring_out; out_vs = MSA_RING; out_mask = MSA_RING - 1; out_add = 0; out_lim = 1 << 30;
           }
           if (snk != SNK_NONE) {
             StripeGeom gn;
             stripe_geom(ks + 1, m, n, kp.band, gn);
             out_cs = gn.cs;
           }
-          {
-            // c_hi of the producer row above (input masking, banded)
-            if (ks > 0) {
-              StripeGeom gp;
-              stripe_geom(ks - 1, m, n, kp.band, gp);
-              out_chi = gp.c_hi;
-            } else {
-              out_chi = n;
-            }
+          if (ks > 0) {
+            StripeGeom gp;
+            stripe_geom(ks - 1, m, n, kp.band, gp);
+            out_chi = gp.c_hi;  // c_hi of the producer row above (input masking, banded)
+          } else {
+            out_chi = n;
           }
-          g_in = (src == SRC_GLOBAL) ? a.gbuf + (size_t)(group - 1) * NC * a.gbuf_stride : nullptr;
           g_out = (snk == SNK_GLOBAL) ? a.gbuf + (size_t)group * NC * a.gbuf_stride : nullptr;
-          if constexpr (OUT == MSA_OUT_DIR) obase = (size_t)pd.out_off + (size_t)ks * pd.pmax * MSA_K * 64;
-          else obase = (size_t)pd.out_off + (size_t)ks * pd.pmax * MSA_K * 64;
-          in_base = 0;
-          if (src == SRC_GLOBAL) {
-            // prefetch phases 0,1,2 (synchronous start)
-#pragma unroll
-            for (int v = 0; v < NC; ++v) {
-              const int c0 = sg.cs + (lane & 15);
-              G0[v] = gload(g_in + (size_t)v * a.gbuf_stride + min(c0, a.gbuf_stride - 1 - MSA_GOFF) + MSA_GOFF);
-              G1[v] = gload(g_in + (size_t)v * a.gbuf_stride + min(c0 + 16, a.gbuf_stride - 1 - MSA_GOFF) + MSA_GOFF);
-              G2[v] = gload(g_in + (size_t)v * a.gbuf_stride + min(c0 + 32, a.gbuf_stride - 1 - MSA_GOFF) + MSA_GOFF);
-            }
-          }
+          obase = (size_t)pd.out_off + (size_t)ks * pd.pmax * MSA_K * 64;
         }
         if (ph >= Tc) {
           const int q = ph - Tc;
-          // ---- global input: verify + stage phase q into ring_in ----
-          if (src == SRC_GLOBAL) {
-            const int col = sg.cs + 16 * q + (lane & 15);
-            const bool need = (lane < 16) && (col <= out_chi) && (col <= n);
-#pragma unroll
-            for (int v = 0; v < NC; ++v) {
-              unsigned long long gv = G0[v];
-              // wave-uniform spin: every lane re-polls until all needed tags match
-              bool ok = !need || ((unsigned)(gv >> 32) == ep);
-              unsigned spins = 0;
-              while (!__all(ok)) {
-                __builtin_amdgcn_s_sleep(1);
-                const unsigned long long r = gload(g_in + (size_t)v * a.gbuf_stride + col + MSA_GOFF);
-                gv = ok ? gv : r;
-                ok = !need || ((unsigned)(gv >> 32) == ep);
-                if (++spins > (1u << 24)) {
-                  if (lane == 0) atomicExch(a.err, 1);
-                  break;
-                }
-              }
-              if (lane < 16) ring_in[v * MSA_RING + ((16 * q + lane) & (MSA_RING - 1))] = (int)(unsigned)gv;
-              asm volatile("" ::: "memory");  // keep the staging write ahead of the int4 reads below
-              G0[v] = G1[v];
-              G1[v] = G2[v];
-              // unconditional prefetch (address clamped into the buffer) so no wait is forced here
-              const int cpre = min(sg.cs + 16 * (q + 3) + (lane & 15), a.gbuf_stride - 1 - MSA_GOFF);
-              G2[v] = gload(g_in + (size_t)v * a.gbuf_stride + cpre + MSA_GOFF);
-            }
-          }
-          const bool masked = (16 * q < sg.mask_lo) || (16 * q + 15 > sg.mask_hi);
-          const bool inmask = (sg.cs + 16 * q + 15 > out_chi);
-          // code words for this phase: 16 bytes = 4 dwords
-          unsigned cw[4];
-          {
-            const unsigned* cp = codes + L.cw_base + 4 * q;
-            cw[0] = cp[0]; cw[1] = cp[1]; cw[2] = cp[2]; cw[3] = cp[3];
-          }
-          unsigned dirw[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            // inputs for 4 steps
-            int IN[NC][4];
-            if (src == SRC_BORDER) {
-#pragma unroll
-              for (int kk = 0; kk < 4; ++kk) {
-                int bv[3];
-                border_top<ALG>(kp, sg.cs + 16 * q + 4 * u + kk, bv);
-#pragma unroll
-                for (int v = 0; v < NC; ++v) IN[v][kk] = bv[v];
-              }
-            } else {
-              const int* base = in_ptr + ((16 * q + 4 * u) & in_mask);
+          const bool masked = uni((16 * q < sg.mask_lo) || (16 * q + 15 > sg.mask_hi));
+          const bool inmask = uni(sg.cs + 16 * q + 15 > out_chi);
+          auto run_phase = [&](auto MASKED_, auto INMASK_) {
+            constexpr bool MASKED = decltype(MASKED_)::value;
+            constexpr bool INMASK = decltype(INMASK_)::value;
+            // ---- all LDS reads of the phase up front (one exposed latency per phase) ----
+            int IN[NC][16];
+            {
+              const int* base = in_ptr + ((16 * q) & in_mask);
 #pragma unroll
               for (int v = 0; v < NC; ++v) {
-                const int4 x = *reinterpret_cast<const int4*>(base + v * in_vs);
-                IN[v][0] = x.x; IN[v][1] = x.y; IN[v][2] = x.z; IN[v][3] = x.w;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                  const int4 x = *reinterpret_cast<const int4*>(base + v * in_vs + 4 * u);
+                  IN[v][4 * u + 0] = x.x; IN[v][4 * u + 1] = x.y; IN[v][4 * u + 2] = x.z; IN[v][4 * u + 3] = x.w;
+                }
               }
-              if (inmask) {
+              if constexpr (INMASK) {
 #pragma unroll
-                for (int kk = 0; kk < 4; ++kk) {
-                  const bool o = sg.cs + 16 * q + 4 * u + kk > out_chi;
+                for (int k = 0; k < 16; ++k) {
+                  const bool o = sg.cs + 16 * q + k > out_chi;
 #pragma unroll
-                  for (int v = 0; v < NC; ++v) IN[v][kk] = o ? MSA_NEG : IN[v][kk];
+                  for (int v = 0; v < NC; ++v) IN[v][k] = o ? MSA_NEG : IN[v][k];
                 }
               }
             }
-            const unsigned s4 = __builtin_amdgcn_perm(L.phi, L.plo, cw[u]);
-            int hist[NC][4];
-            unsigned dq = 0;
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk) {
-              const int t = 16 * q + 4 * u + kk;
-              const int s = ((int)(s4 << (24 - 8 * kk))) >> 24;
-              int inv[3];
-#pragma unroll
-              for (int v = 0; v < NC; ++v) inv[v] = IN[v][kk];
-              int cr[3];
-              unsigned d;
-              if (masked) d = step<ALG, OUT, true, TRACKPOS>(kp, L, inv, s, t, cr);
-              else d = step<ALG, OUT, false, TRACKPOS>(kp, L, inv, s, t, cr);
-#pragma unroll
-              for (int v = 0; v < NC; ++v) hist[v][kk] = cr[v];
-              dq |= d << (8 * kk);
+            unsigned cw[4];
+            {
+              const unsigned* cp = codes + L.cw_base + 4 * q;
+              cw[0] = cp[0]; cw[1] = cp[1]; cw[2] = cp[2]; cw[3] = cp[3];
             }
-            dirw[u] = dq;
-            // cell outputs
-            const size_t qi = (size_t)(4 * q + u) * 64 + lane;  // int4 index within stripe block
-            if constexpr (OUT == MSA_OUT_H) {
-              int4 hv;
-              if constexpr (ALG == MSA_ALG_REF || ALG == MSA_ALG_PART) {
-                hv = make_int4(imax3(hist[0][0], hist[1][0], hist[2][0]), imax3(hist[0][1], hist[1][1], hist[2][1]),
-                               imax3(hist[0][2], hist[1][2], hist[2][2]), imax3(hist[0][3], hist[1][3], hist[2][3]));
-              } else {
-                hv = make_int4(hist[0][0], hist[0][1], hist[0][2], hist[0][3]);
+            int hist[NC][16];
+            unsigned dirw[4] = {0u, 0u, 0u, 0u};
+            int4* hrow = reinterpret_cast<int4*>(a.outH + obase) + (size_t)(4 * q) * 64 + lane;
+            int4* t2row = reinterpret_cast<int4*>(a.outT2 + obase) + (size_t)(4 * q) * 64 + lane;
+            int4* t3row = reinterpret_cast<int4*>(a.outT3 + obase) + (size_t)(4 * q) * 64 + lane;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const unsigned s4 = __builtin_amdgcn_perm(L.phi, L.plo, cw[u]);
+              unsigned dq = 0;
+#pragma unroll
+              for (int kk = 0; kk < 4; ++kk) {
+                const int k = 4 * u + kk;
+                const int t = 16 * q + k;
+                const int s = ((int)(s4 << (24 - 8 * kk))) >> 24;
+                int inv[3];
+#pragma unroll
+                for (int v = 0; v < NC; ++v) inv[v] = IN[v][k];
+                int cr[3];
+                const unsigned d = step<ALG, OUT, MASKED, TRACKPOS>(kp, L, inv, s, t, cr);
+#pragma unroll
+                for (int v = 0; v < NC; ++v) hist[v][k] = cr[v];
+                dq |= d << (8 * kk);
               }
-              reinterpret_cast<int4*>(a.outH + obase)[qi] = hv;
-            } else if constexpr (OUT == MSA_OUT_TAB) {
-              reinterpret_cast<int4*>(a.outH + obase)[qi] = make_int4(hist[0][0], hist[0][1], hist[0][2], hist[0][3]);
-              reinterpret_cast<int4*>(a.outT2 + obase)[qi] = make_int4(hist[1][0], hist[1][1], hist[1][2], hist[1][3]);
-              reinterpret_cast<int4*>(a.outT3 + obase)[qi] = make_int4(hist[2][0], hist[2][1], hist[2][2], hist[2][3]);
+              dirw[u] = dq;
+              // cell outputs: one 1 KiB coalesced store per wave per 4 steps
+              if constexpr (OUT == MSA_OUT_H) {
+                int4 hv;
+                if constexpr (ALG == MSA_ALG_REF || ALG == MSA_ALG_PART) {
+                  hv = make_int4(imax3(hist[0][4 * u], hist[1][4 * u], hist[2][4 * u]),
+                                 imax3(hist[0][4 * u + 1], hist[1][4 * u + 1], hist[2][4 * u + 1]),
+                                 imax3(hist[0][4 * u + 2], hist[1][4 * u + 2], hist[2][4 * u + 2]),
+                                 imax3(hist[0][4 * u + 3], hist[1][4 * u + 3], hist[2][4 * u + 3]));
+                } else {
+                  hv = make_int4(hist[0][4 * u], hist[0][4 * u + 1], hist[0][4 * u + 2], hist[0][4 * u + 3]);
+                }
+                hrow[u * 64] = hv;
+              } else if constexpr (OUT == MSA_OUT_TAB) {
+                hrow[u * 64] = make_int4(hist[0][4 * u], hist[0][4 * u + 1], hist[0][4 * u + 2], hist[0][4 * u + 3]);
+                t2row[u * 64] = make_int4(hist[1][4 * u], hist[1][4 * u + 1], hist[1][4 * u + 2], hist[1][4 * u + 3]);
+                t3row[u * 64] = make_int4(hist[2][4 * u], hist[2][4 * u + 1], hist[2][4 * u + 2], hist[2][4 * u + 3]);
+              }
             }
-            // hand the bottom row to the next stripe (lane 63)
+            if constexpr (OUT == MSA_OUT_DIR) {
+              reinterpret_cast<uint4*>(a.outDir + obase)[(size_t)q * 64 + lane] =
+                  make_uint4(dirw[0], dirw[1], dirw[2], dirw[3]);
+            }
+            // hand the bottom row to the next stripe: lane 63, once per phase
             if (snk != SNK_NONE && lane == 63) {
-              const int x = (sg.cs + 16 * q + 4 * u - 63 - out_cs + out_add) & out_mask;  // multiple of 4
-              if (x >= 0 && x <= out_lim) {
+              const int x = (sg.cs + 16 * q - 63 - out_cs + out_add) & out_mask;  // multiple of 16
+              if (x >= 0 && x + 12 <= out_lim) {
                 int* dst = out_ptr + x;
 #pragma unroll
                 for (int v = 0; v < NC; ++v)
-                  *reinterpret_cast<int4*>(dst + v * out_vs) = make_int4(hist[v][0], hist[v][1], hist[v][2], hist[v][3]);
+#pragma unroll
+                  for (int u = 0; u < 4; ++u)
+                    *reinterpret_cast<int4*>(dst + v * out_vs + 4 * u) =
+                        make_int4(hist[v][4 * u], hist[v][4 * u + 1], hist[v][4 * u + 2], hist[v][4 * u + 3]);
               }
             }
-          }
-          if constexpr (OUT == MSA_OUT_DIR) {
-            reinterpret_cast<uint4*>(a.outDir + obase)[(size_t)q * 64 + lane] = make_uint4(dirw[0], dirw[1], dirw[2], dirw[3]);
-          }
-          // global sink: granules for the 16 columns produced this phase
-          if (snk == SNK_GLOBAL) {
-            asm volatile("" ::: "memory");  // lane 63's int4 ring writes stay ahead of these reads
-            if (lane < 16) {
-              const int x = sg.cs + 16 * q - 63 - out_cs + lane;
-              const int col = sg.cs + 16 * q - 63 + lane;
-              if (col + MSA_GOFF >= 0 && col + MSA_GOFF < a.gbuf_stride) {
-#pragma unroll
-                for (int v = 0; v < NC; ++v) {
+            // global sink: 8-byte {epoch, value} granules for the 16 columns of this phase
+            if (snk == SNK_GLOBAL) {
+              asm volatile("" ::: "memory");  // lane 63's ring writes stay ahead of these reads
+              const int v = lane >> 4, l = lane & 15;
+              if (v < NC) {
+                const int x = sg.cs + 16 * q - 63 - out_cs + l;
+                const int col = sg.cs + 16 * q - 63 + l;
+                if (col + MSA_GOFF >= 0 && col + MSA_GOFF < a.gbuf_stride) {
                   const int val = ring_out[v * MSA_RING + (x & (MSA_RING - 1))];
                   gstore(g_out + (size_t)v * a.gbuf_stride + col + MSA_GOFF,
                          ((unsigned long long)ep << 32) | (unsigned)val);
                 }
               }
             }
+          };
+          using T_ = std::true_type;
+          using F_ = std::false_type;
+          if (inmask) {
+            if (masked) run_phase(T_{}, T_{}); else run_phase(F_{}, T_{});
+          } else {
+            if (masked) run_phase(T_{}, F_{}); else run_phase(F_{}, F_{});
           }
           if (q == sg.P - 1) {
             // ---- stripe finalize ----

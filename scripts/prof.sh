@@ -1,0 +1,9 @@
+#!/bin/bash
+# usage: scripts/prof.sh <workload> <outdir>   (run on the GPU box)
+set -e
+WL=${1:-c2}; OUT=${2:-gpurun_out/prof}
+export TMPDIR=/tmp
+mkdir -p $OUT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 scripts/prof_run.py $WL 5
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES -d $OUT/pmc1 -o run --output-format csv -- python3 scripts/prof_run.py $WL 2
+timeout -k 10 300 rocprofv3 --pmc SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_SCA -d $OUT/pmc2 -o run --output-format csv -- python3 scripts/prof_run.py $WL 2
