@@ -118,6 +118,7 @@ struct msa_plan {
   unsigned long long* d_sum = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   uint32_t epoch = 0;
+  unsigned long long* stamps = nullptr;  // diagnostic build
 };
 
 extern "C" {
@@ -349,6 +350,7 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
   else a.outH = (int32_t*)c0;
   a.outT2 = (int32_t*)c1;
   a.outT3 = (int32_t*)c2;
+  a.stamps = P->stamps;
   HIPCHK(hipMemsetAsync(P->d_ticket, 0, 64, st));
   HIPCHK(hipEventRecord(P->ev0, st));
   hipLaunchKernelGGL(P->fn, dim3(P->grid), dim3(MSA_THREADS), P->lds_bytes, st, a);
@@ -361,6 +363,10 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
   HIPCHK(hipGetLastError());
   return MSA_OK;
 }
+
+#ifdef MSA_STAMPS
+extern "C" int msa_debug_stamps(msa_plan* P, unsigned long long* d) { P->stamps = d; return 0; }
+#endif
 
 int msa_plan_last_kernel_ms(msa_plan* P, float* ms) {
   if (!P || !ms) return MSA_ERR_ARG;

@@ -114,6 +114,7 @@ struct KArgs {
   int32_t* outT2;            // O_TAB planes
   int32_t* outT3;
   uint8_t* outDir;           // O_DIR
+  unsigned long long* stamps;  // diagnostic build only (MSA_STAMPS): per-phase s_memtime
 };
 
 template <int ALG>
@@ -538,6 +539,12 @@ __global__ __launch_bounds__(MSA_THREADS) void stripe_kernel(KArgs a) {
     __syncthreads();  // pairs with the loader's post-staging barrier
 
     for (int ph = 0; ph < total; ++ph) {
+#ifdef MSA_STAMPS
+      if (a.stamps && item == 0 && w == 2 && ph < 4096) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+        if (lane == 0) a.stamps[3 * ph] = t0;
+      }
+#endif
       if (cur < ns) {
         const int Tc = uni(sched[cur].T);
         if (ph == Tc) {
@@ -766,7 +773,20 @@ __global__ __launch_bounds__(MSA_THREADS) void stripe_kernel(KArgs a) {
           }
         }
       }
+#ifdef MSA_STAMPS
+      if (a.stamps && item == 0 && w == 2 && ph < 4096) {
+        __builtin_amdgcn_s_waitcnt(0);
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+        if (lane == 0) a.stamps[3 * ph + 1] = t1;
+      }
+#endif
       __syncthreads();
+#ifdef MSA_STAMPS
+      if (a.stamps && item == 0 && w == 2 && ph < 4096) {
+        const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+        if (lane == 0) a.stamps[3 * ph + 2] = t2;
+      }
+#endif
     }
   }
 }

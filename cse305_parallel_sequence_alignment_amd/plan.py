@@ -154,13 +154,28 @@ class Plan:
         return out
 
 
-def stripe_phases(k: int, m: int, n: int, band: int) -> int:
-    """Python restatement of stripe_geom().P (msa_kernels.hip) for host layout sizing."""
+def jlo_of(i: int, band: int) -> int:
+    return 1 if band < 0 else max(1, i - band)
+
+
+def jhi_of(i: int, n: int, band: int) -> int:
+    return n if band < 0 else min(n, i + band)
+
+
+def stripe_geom(k: int, m: int, n: int, band: int):
+    """Python restatement of stripe_geom() (msa_kernels.hip): (cs, P) of pair-local stripe k.
+
+    Lane r of stripe k (row 64k+r+1) processes column cs + t - r at step t,
+    t in [0, 16P); cs is chosen so that cs = c_lo - lead with
+    lead = 1 + ((c_lo - 1 - k) mod 16), which 16-aligns producer/consumer ring I/O."""
     i0 = 64 * k + 1
     rlast = min(63, m - 64 * k - 1)
     ilast = i0 + rlast
-    jlo = 1 if band < 0 else max(1, i0 - band)
-    lead = (jlo - 1 - k) % 16 + 1
-    cs = jlo - lead
-    jhi = n if band < 0 else min(n, ilast + band)
-    return (jhi - cs + rlast) // 16 + 1
+    clo = jlo_of(i0, band)
+    lead = (clo - 1 - k) % 16 + 1
+    cs = clo - lead
+    return cs, (jhi_of(ilast, n, band) - cs + rlast) // 16 + 1
+
+
+def stripe_phases(k: int, m: int, n: int, band: int) -> int:
+    return stripe_geom(k, m, n, band)[1]

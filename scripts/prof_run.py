@@ -10,7 +10,11 @@ wl = sys.argv[1] if len(sys.argv) > 1 else "c2"
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 seqs = load_dataset()[1]
 enc = lambda s: torch.from_numpy(np.frombuffer(s.translate(bytes.maketrans(b"ACGT", b"\x00\x01\x02\x03")), dtype=np.uint8).copy()).cuda()
-if wl == "c2":
+if wl == "c2n":
+    A, B = seqs[1][:10000], seqs[0][:10000]
+    pl = Plan(LB.SW_LINEAR, LB.CELLS_NONE, [10000], [10000], [0], [0], match=1, mismatch=0, gap_open=1, gap_extend=1)
+    out = None
+elif wl == "c2":
     A, B = seqs[1][:10000], seqs[0][:10000]
     pl = Plan(LB.SW_LINEAR, LB.CELLS_H, [10000], [10000], [0], [0], match=1, mismatch=0, gap_open=1, gap_extend=1)
     out = torch.empty(pl.cells_elems, dtype=torch.int32, device="cuda")

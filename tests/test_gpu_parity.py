@@ -1,0 +1,220 @@
+"""Bit-exact parity of the HIP stripe kernels (through libmsa.so's C-ABI) with the oracle and golden fixtures.
+
+Integer DP: every comparison is exact (scores, end cells, full H matrices,
+direction-derived tracebacks, node lists, stdout text)."""
+import hashlib
+import json
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+ACGT = np.frombuffer(b"ACGT", dtype=np.uint8)
+
+
+def enc(s: bytes) -> np.ndarray:
+    return np.frombuffer(s.translate(bytes.maketrans(b"ACGT", b"\x00\x01\x02\x03")), dtype=np.uint8).copy()
+
+
+def rs(rng, n):
+    return rng.choice(ACGT, n).tobytes()
+
+
+def _dev(x, dev):
+    import torch
+
+    return torch.from_numpy(enc(x)).to(dev)
+
+
+@pytest.fixture(scope="module")
+def LB():
+    from cse305_parallel_sequence_alignment_amd import _lib
+
+    return _lib
+
+
+@pytest.mark.parametrize("single", [True, False])
+def test_sw_linear_H_small(oracle, dev, LB, single):
+    import torch
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+
+    rng = np.random.default_rng(7)
+    for (m, n) in [(1, 1), (5, 7), (64, 64), (65, 100), (130, 70), (200, 513), (511, 300), (700, 650), (520, 40)]:
+        A, B = rs(rng, m), rs(rng, n)
+        pl = Plan(LB.SW_LINEAR, LB.CELLS_H, [m], [n], [0], [0], match=2, mismatch=-1, gap_open=1, gap_extend=1,
+                  track_end=True, single=single)
+        H = torch.empty(pl.cells_elems, dtype=torch.int32, device=dev)
+        pl.run(_dev(A, dev), _dev(B, dev), H)
+        res = pl.results()[0]
+        Hd = pl.deskew(H.cpu().numpy(), 0, pl.stripe_meta())
+        o = oracle.sw(A, B, 2, -1, 1, 1, want_h=True)
+        assert (res["score"], tuple(res["end"])) == (o["score"], tuple(o["end"])), (m, n)
+        assert np.array_equal(Hd[1:, 1:], o["H"][1:, 1:]), (m, n)
+        assert pl.checksum(H) == oracle.checksum_h(o["H"])
+
+
+def test_sw_linear_single_multi_group(oracle, dev, LB):
+    """Single-pair mode across several workgroups (cross-WG row handoff), repeated launches."""
+    import torch
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+
+    rng = np.random.default_rng(11)
+    for (m, n) in [(1500, 1200), (3000, 2500)]:
+        A, B = rs(rng, m), rs(rng, n)
+        pl = Plan(LB.SW_LINEAR, LB.CELLS_H, [m], [n], [0], [0], match=2, mismatch=-1, gap_open=1, gap_extend=1,
+                  track_end=True, single=True)
+        H = torch.empty(pl.cells_elems, dtype=torch.int32, device=dev)
+        dA, dB = _dev(A, dev), _dev(B, dev)
+        o = oracle.sw(A, B, 2, -1, 1, 1, want_h=True)
+        for _ in range(3):
+            pl.run(dA, dB, H)
+            res = pl.results()[0]
+            assert res["score"] == o["score"] and tuple(res["end"]) == tuple(o["end"])
+            assert pl.checksum(H) == oracle.checksum_h(o["H"])
+
+
+def test_sw_linear_batch_ragged(oracle, dev, LB):
+    import torch
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+
+    rng = np.random.default_rng(11)
+    sizes = [(1100, 1000), (600, 4000), (1300, 960), (64, 3000), (2000, 1500), (33, 17), (1, 5), (129, 1)]
+    As = [rs(rng, m) for m, n in sizes]
+    Bs = [rs(rng, n) for m, n in sizes]
+    ao = np.cumsum([0] + [m for m, n in sizes])[:-1]
+    bo = np.cumsum([0] + [n for m, n in sizes])[:-1]
+    pl = Plan(LB.SW_LINEAR, LB.CELLS_H, [m for m, n in sizes], [n for m, n in sizes], ao, bo, match=2, mismatch=-1,
+              gap_open=1, gap_extend=1, track_end=True, single=False)
+    H = torch.empty(pl.cells_elems, dtype=torch.int32, device=dev)
+    pl.run(_dev(b"".join(As), dev), _dev(b"".join(Bs), dev), H)
+    res, meta, Hh = pl.results(), pl.stripe_meta(), H.cpu().numpy()
+    for k, (m, n) in enumerate(sizes):
+        o = oracle.sw(As[k], Bs[k], 2, -1, 1, 1, want_h=True)
+        assert res[k]["score"] == o["score"] and tuple(res[k]["end"]) == tuple(o["end"]), (m, n)
+        assert np.array_equal(pl.deskew(Hh, k, meta)[1:, 1:], o["H"][1:, 1:]), (m, n)
+
+
+def test_sw_linear_c4_shape_scores(oracle, dev, LB):
+    """C4's shape (4,000 x 4,000 pairs, score only) on a 64-pair batch; spot-checked against the oracle."""
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+
+    rng = np.random.default_rng(4)
+    L, K = 4000, 64
+    As = [rs(rng, L) for _ in range(K)]
+    B = rs(rng, L)
+    pl = Plan(LB.SW_LINEAR, LB.CELLS_NONE, [L] * K, [L] * K, [k * L for k in range(K)], [0] * K, match=1,
+              mismatch=0, gap_open=1, gap_extend=1, single=False)
+    pl.run(_dev(b"".join(As), dev), _dev(B, dev))
+    res = pl.results()
+    for k in (0, 1, 31, 63):
+        assert res[k]["score"] == oracle.sw(As[k], B, 1, 0, 1, 1)["score"]
+
+
+def test_main_alignment_kat_and_harness(oracle, dev, dataset):
+    """main_alignment_function stdout (main_alignment.cpp:353-410) byte-exact on the KAT and harness pairs."""
+    from cse305_parallel_sequence_alignment_amd import api
+
+    kat = json.loads((GOLDEN / "kat.json").read_text())
+    t, sc = api.main_alignment_text(b"-AGGA", b"-AGTGC", 4, 5, 3, 1, 2)
+    assert t == "bp1\nbp1.2\nbp2\nbp3\nbp4\nAG-GA\nAGTGC\n"
+    _, seqs = dataset
+    lines = []
+    for hp in kat["harness"]:
+        A, B = seqs[hp["a"]][: hp["L"]], seqs[hp["b"]][: hp["L"]]
+        t, sc = api.main_alignment_text(b"\0" + A, b"\0" + B, hp["L"], hp["L"], 32, 1, 2)
+        assert hashlib.md5(t.encode()).hexdigest() == hp["stdout_md5"] and sc == hp["score"]
+        if hp["L"] == 1000:
+            lines += t.split("\n")[5:7]
+    assert hashlib.md5(("\n".join(lines) + "\n").encode()).hexdigest() == kat["harness_1k_lines_md5"]
+    for pr in kat["seq0_seq1_prefixes"]:
+        L = pr["L"]
+        t, sc = api.main_alignment_text(b"\0" + seqs[0][:L], b"\0" + seqs[1][:L], L, L, 32, 1, 2)
+        l = t.split("\n")[5:7]
+        assert sc == pr["score"]
+        assert hashlib.md5((l[0] + "\n" + l[1] + "\n").encode()).hexdigest() == pr["lines_md5"]
+
+
+def test_subproblem_fixtures(dev):
+    """Subproblem::compute_tables + find_alignment on all 41 fixtures (every start/end type, g/h)."""
+    from cse305_parallel_sequence_alignment_amd import api
+
+    paths = json.loads((GOLDEN / "subproblem_paths.json").read_text())
+    tabs = np.load(GOLDEN / "subproblem_tables.npz")
+    for c in paths:
+        A, B = c["A"].encode(), c["B"].encode()
+        sp = api.Subproblem(b"\0" + A, b"\0" + B, len(A), len(B), 0, 0, 1, c["start"], c["end"], c["g"], c["h"])
+        sp.compute_tables()
+        if c["key"] + "_T" in tabs:
+            for x, y in zip(sp._tables_int, tabs[c["key"] + "_T"]):
+                assert np.array_equal(x, y), c["key"]
+        sp.find_alignment()
+        assert sp.alignment_list() == [tuple(x) for x in c["nodes"]], c["key"]
+        assert sp.alignment_end.as_tuple() == tuple(c["end_node"]), c["key"]
+
+
+def test_partial_fixtures(oracle, dev, dataset):
+    """findPartialBalancedPartitionParallel (partial.cpp:149-163, int32 wrap) on the 80 fixtures + tables."""
+    from cse305_parallel_sequence_alignment_amd import api
+
+    for c in json.loads((GOLDEN / "partial.json").read_text()):
+        A, B = c["A"].encode(), c["B"].encode()
+        got = [a.as_tuple() for a in api.findPartialBalancedPartitionParallel(A, B, len(A), len(B), c["p"], c["g"],
+                                                                               c["h"], c["start"], c["end"])]
+        assert got == [tuple(x) for x in c["partition"]]
+    _, seqs = dataset
+    T, R = api.partial_tables(seqs[0][:40], seqs[1][:40], 40, 40, 1, 2, 1, 1)
+    To, Ro = oracle.partial_tables(seqs[0][:40], seqs[1][:40], 1, 2, 1, 1)
+    for a, b in zip(T + R, To + Ro):
+        assert np.array_equal(a, b)
+
+
+def test_sw_affine_traceback(oracle, dev):
+    from cse305_parallel_sequence_alignment_amd import api
+
+    rng = np.random.default_rng(3)
+    for (m, n) in [(30, 40), (100, 90), (300, 257), (700, 800), (1, 1), (64, 1)]:
+        A, B = rs(rng, m), rs(rng, n)
+        for (ma, mi, go, ge) in [(1, 0, 1, 1), (2, -3, 5, 2), (1, -1, 3, 1)]:
+            r = api.sw_align(A, B, ma, mi, go, ge)
+            o = oracle.sw(A, B, ma, mi, go, ge, want_tb=True)
+            assert (r["score"], r["end"], r["beg"], r["cigar"]) == (o["score"], o["end"], o["beg"], o["cigar"])
+
+
+def test_sw_linear_10k_property(oracle, dev, LB, dataset):
+    """C2 size (10k x 10k): score/end equal the oracle, H checksum equals the oracle's checksum-of-cells."""
+    import torch
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+
+    _, seqs = dataset
+    A, B = seqs[1][:10000], seqs[0][:10000]
+    pl = Plan(LB.SW_LINEAR, LB.CELLS_H, [10000], [10000], [0], [0], match=1, mismatch=0, gap_open=1, gap_extend=1,
+              track_end=True)
+    H = torch.empty(pl.cells_elems, dtype=torch.int32, device=dev)
+    pl.run(_dev(A, dev), _dev(B, dev), H)
+    o = oracle.sw(A, B, 1, 0, 1, 1, want_h=True)
+    res = pl.results()[0]
+    assert res["score"] == o["score"] and tuple(res["end"]) == tuple(o["end"])
+    assert pl.checksum(H) == oracle.checksum_h(o["H"])
+
+
+@pytest.mark.parametrize("m,n,w", [(300, 290, 32), (1000, 1000, 64), (1500, 1490, 512), (700, 700, 1)])
+def test_nw_banded_reference_gotoh(oracle, dev, LB, m, n, w):
+    """C3's kernel (banded reference Gotoh, g=1 h=2) at small sizes: every in-band H cell and the score."""
+    import torch
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+
+    rng = np.random.default_rng(m + w)
+    A, B = rs(rng, m), rs(rng, n)
+    pl = Plan(LB.NW_BANDED, LB.CELLS_H, [m], [n], [0], [0], match=1, mismatch=0, gap_open=3, gap_extend=1, band=w)
+    H = torch.empty(pl.cells_elems, dtype=torch.int32, device=dev)
+    pl.run(_dev(A, dev), _dev(B, dev), H)
+    score, Ho = oracle.banded_ref(A, B, w, 1.0, 2.0, want_h=True)
+    Hd = pl.deskew(H.cpu().numpy(), 0, pl.stripe_meta())
+    i, j = np.indices(Ho.shape)
+    inb = (np.abs(i - j) <= w) & (i > 0) & (j > 0)
+    assert np.array_equal(Hd[inb], Ho[inb])
+    assert pl.checksum(H) == oracle.checksum_h(Ho, w)
+    assert pl.results()[0]["score"] == int(score)

@@ -1,0 +1,98 @@
+"""The oracle pinned against the reference's own outputs (CPU).
+
+Fixtures in tests/golden/ were produced by tests/golden/make_golden.py from
+the reference's unmodified subproblem_alignment.cpp / partial.cpp compiled
+into oracle/_ref; the two KATs are the reference's own
+hand-worked examples (testing.cpp / README).  When oracle/_ref is present
+(build container) the restatement is also cross-checked against it live.
+"""
+import hashlib
+import json
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+KAT = json.loads((GOLDEN / "kat.json").read_text())
+PATHS = json.loads((GOLDEN / "subproblem_paths.json").read_text())
+PARTS = json.loads((GOLDEN / "partial.json").read_text())
+
+
+def test_kat_agga_agtgc(oracle):
+    # main_alignment.cpp:353-410 on the reference's own example (1-based buffers)
+    text, score = oracle.main_alignment_text(b"AGGA", b"AGTGC", 1.0, 2.0)
+    assert text == "bp1\nbp1.2\nbp2\nbp3\nbp4\nAG-GA\nAGTGC\n"
+    k = KAT["AGGA_AGTGC_g1_h2"]
+    assert score == k["score"]
+    r = oracle.subproblem_align(b"AGGA", b"AGTGC", -1, -1, 1.0, 2.0)
+    assert [list(x) for x in r["nodes"]] == k["nodes"]
+
+
+def test_kat_agga_atgtc(oracle):
+    k = KAT["AGGA_ATGTC_g2_h1"]
+    r = oracle.subproblem_align(k["A"].encode(), k["B"].encode(), -1, -1, k["g"], k["h"])
+    assert [list(x) for x in r["nodes"]] == k["nodes"]
+
+
+def test_harness_pairs_stdout(oracle, dataset):
+    """testing.cpp:112-140: the four 1000-bp harness alignments, exact stdout."""
+    _, seqs = dataset
+    lines = []
+    for hp in KAT["harness"]:
+        A, B = seqs[hp["a"]][: hp["L"]], seqs[hp["b"]][: hp["L"]]
+        text, score = oracle.main_alignment_text(A, B, 1.0, 2.0)
+        assert hashlib.md5(text.encode()).hexdigest() == hp["stdout_md5"]
+        assert score == hp["score"]
+        if hp["L"] == 1000:
+            lines += text.split("\n")[5:7]
+    assert hashlib.md5(("\n".join(lines) + "\n").encode()).hexdigest() == KAT["harness_1k_lines_md5"]
+
+
+def test_prefix_scores_and_checksums(oracle, dataset):
+    _, seqs = dataset
+    for pr in KAT["seq0_seq1_prefixes"]:
+        L = pr["L"]
+        text, score = oracle.main_alignment_text(seqs[0][:L], seqs[1][:L], 1.0, 2.0)
+        l = text.split("\n")[5:7]
+        assert score == pr["score"]
+        assert hashlib.md5((l[0] + "\n" + l[1] + "\n").encode()).hexdigest() == pr["lines_md5"]
+
+
+@pytest.mark.parametrize("case", PATHS, ids=[c["key"] for c in PATHS])
+def test_subproblem_tables_and_paths(oracle, case):
+    tabs = np.load(GOLDEN / "subproblem_tables.npz")
+    A, B = case["A"].encode(), case["B"].encode()
+    r = oracle.subproblem_align(A, B, case["start"], case["end"], case["g"], case["h"])
+    assert [tuple(x) for x in r["nodes"]] == [tuple(x) for x in case["nodes"]]
+    assert tuple(r["end"]) == tuple(case["end_node"])
+    if case["key"] + "_T" in tabs:
+        T = tabs[case["key"] + "_T"]
+        T1, T2, T3, inv = oracle.subproblem_tables(A, B, case["start"], case["g"], case["h"])
+        assert inv == case["invert"]
+        for got, want in zip((T1, T2, T3), T):  # fixtures: int32, INT32_MIN where the reference holds -inf
+            assert np.array_equal(np.where(np.isinf(got), np.iinfo(np.int32).min, got).astype(np.int32), want)
+
+
+@pytest.mark.parametrize("k", range(len(PARTS)))
+def test_partial_partition(oracle, k):
+    c = PARTS[k]
+    got = oracle.partial_partition(c["A"].encode(), c["B"].encode(), c["p"], c["g"], c["h"], c["start"], c["end"])
+    assert got == [tuple(x) for x in c["partition"]]
+
+
+@pytest.mark.skipif("not __import__('oracle.oracle', fromlist=['x']).ref_available()",
+                    reason="oracle/_ref not built (reference sources absent)")
+def test_restatement_vs_reference_live(oracle):
+    """Random small cases: C restatement == the reference's own code (oracle/_ref)."""
+    rng = np.random.default_rng(99)
+    for _ in range(12):
+        m, n = rng.integers(1, 60, size=2)
+        A = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), m).tobytes()
+        B = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), n).tobytes()
+        st, en = rng.choice([-1, -2, -3, 1, 2, 3], size=2)
+        r = oracle.subproblem_align(A, B, int(st), int(en), 1.0, 2.0)
+        ref = oracle.ref_subproblem(A, B, int(st), int(en), 1.0, 2.0)
+        assert [tuple(x) for x in r["nodes"]] == [tuple(x) for x in ref["nodes"]]
+        p = int(rng.integers(1, 6))
+        assert oracle.partial_partition(A, B, p, 1.0, 2.0, 1, 1) == oracle.ref_partial(A, B, p, 1.0, 2.0, 1, 1)
