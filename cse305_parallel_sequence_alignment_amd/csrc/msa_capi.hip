@@ -64,10 +64,10 @@ int nc_of(int alg) {
 typedef void (*kfn_t)(KArgs);
 
 template <int ALG, int OUT, bool TP>
-kfn_t kf() { return stripe_kernel<ALG, OUT, TP>; }
+kfn_t kf(int W) { return W == MSA_WAVES_SINGLE ? stripe_kernel<ALG, OUT, TP, MSA_WAVES_SINGLE> : stripe_kernel<ALG, OUT, TP, MSA_WAVES_BATCH>; }
 
-kfn_t pick_kernel(int alg, int out, int tp) {
-#define K3(A, O) return tp ? kf<A, O, true>() : kf<A, O, false>()
+kfn_t pick_kernel(int alg, int out, int tp, int W) {
+#define K3(A, O) return tp ? kf<A, O, true>(W) : kf<A, O, false>(W)
   switch (alg) {
     case MSA_ALG_SWL:
       if (out == MSA_OUT_NONE) K3(MSA_ALG_SWL, MSA_OUT_NONE);
@@ -79,17 +79,17 @@ kfn_t pick_kernel(int alg, int out, int tp) {
       if (out == MSA_OUT_DIR) K3(MSA_ALG_SWA, MSA_OUT_DIR);
       break;
     case MSA_ALG_NWA:
-      if (out == MSA_OUT_NONE) return kf<MSA_ALG_NWA, MSA_OUT_NONE, false>();
-      if (out == MSA_OUT_H) return kf<MSA_ALG_NWA, MSA_OUT_H, false>();
+      if (out == MSA_OUT_NONE) return kf<MSA_ALG_NWA, MSA_OUT_NONE, false>(W);
+      if (out == MSA_OUT_H) return kf<MSA_ALG_NWA, MSA_OUT_H, false>(W);
       break;
     case MSA_ALG_REF:
-      if (out == MSA_OUT_NONE) return kf<MSA_ALG_REF, MSA_OUT_NONE, false>();
-      if (out == MSA_OUT_TAB) return kf<MSA_ALG_REF, MSA_OUT_TAB, false>();
-      if (out == MSA_OUT_DIR) return kf<MSA_ALG_REF, MSA_OUT_DIR, false>();
-      if (out == MSA_OUT_H) return kf<MSA_ALG_REF, MSA_OUT_H, false>();
+      if (out == MSA_OUT_NONE) return kf<MSA_ALG_REF, MSA_OUT_NONE, false>(W);
+      if (out == MSA_OUT_TAB) return kf<MSA_ALG_REF, MSA_OUT_TAB, false>(W);
+      if (out == MSA_OUT_DIR) return kf<MSA_ALG_REF, MSA_OUT_DIR, false>(W);
+      if (out == MSA_OUT_H) return kf<MSA_ALG_REF, MSA_OUT_H, false>(W);
       break;
     case MSA_ALG_PART:
-      if (out == MSA_OUT_TAB) return kf<MSA_ALG_PART, MSA_OUT_TAB, false>();
+      if (out == MSA_OUT_TAB) return kf<MSA_ALG_PART, MSA_OUT_TAB, false>(W);
       break;
   }
 #undef K3
@@ -102,6 +102,7 @@ struct msa_plan {
   msa_plan_desc d;
   msa_kparams kp;
   int nc = 1;
+  int W = MSA_WAVES_BATCH;  // compute waves per workgroup
   std::vector<msa_pair_desc> pairs;
   int64_t total_stripes = 0;
   int64_t cells_elems = 0;
@@ -192,7 +193,9 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     default: delete P; return MSA_ERR_ARG;
   }
   const int tp = (kalg == MSA_ALG_SWL || kalg == MSA_ALG_SWA) ? (desc->track_end ? 1 : 0) : 0;
-  P->fn = pick_kernel(kalg, out_mode, tp);
+  const int W = desc->single ? MSA_WAVES_SINGLE : MSA_WAVES_BATCH;
+  P->W = W;
+  P->fn = pick_kernel(kalg, out_mode, tp, W);
   if (!P->fn) { delete P; return MSA_ERR_UNSUPPORTED; }
   if (desc->single && desc->n_pairs != 1) { delete P; return MSA_ERR_ARG; }
   P->nc = nc_of(kalg);
@@ -219,11 +222,21 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   for (int64_t p = 0; p < desc->n_pairs; ++p) {
     const int64_t m = desc->m[p], n = desc->n[p];
     if (m <= 0 || n <= 0 || m > (1 << 26) || n > (1 << 26)) { delete P; return MSA_ERR_ARG; }
+    if (kalg == MSA_ALG_SWL) {
+      // shifted recurrence G = H + g*(i+j): G must stay far from the -2^30 sentinel
+      // and from int32 overflow; the profile byte holds score + 2g
+      const int64_t g = kp.gap_open;
+      const int64_t top = g * (m + n + 2) + (int64_t)std::max(0, kp.match) * std::min(m, n);
+      if (g < 0 || top >= (int64_t(1) << 29) || kp.match + 2 * g > 127 || kp.mismatch + 2 * g < -128) {
+        delete P;
+        return MSA_ERR_UNSUPPORTED;
+      }
+    }
     if (band >= 0 && std::llabs(m - n) > band) { delete P; return MSA_ERR_ARG; }
     const int S = (int)((m + 63) / 64);
     int pmax = 0;
-    // per-item code window (items = groups of 8 in single mode, whole pair in batch)
-    const int per_item = desc->single ? MSA_WAVES : S;
+    // per-item code window (items = groups of W stripes in single mode, whole pair in batch)
+    const int per_item = desc->single ? W : S;
     for (int k0 = 0; k0 < S; k0 += per_item) {
       int cmin = 1 << 30, cmax = -(1 << 30);
       for (int k = k0; k < std::min(S, k0 + per_item); ++k) {
@@ -252,16 +265,16 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   }
   P->total_stripes = stripe0;
   P->cells_elems = off;
-  kp.sched_cap = desc->single ? MSA_WAVES : max_S;
+  kp.sched_cap = desc->single ? W : max_S;
   kp.lds_code_bytes = ((max_code + 16) + 15) & ~15;
   kp.lds_row_words = desc->single ? 0 : (((max_P * MSA_K + MSA_ROWOFF + 32) + 15) & ~15);
   if (desc->single) {
     const int S = (int)((desc->m[0] + 63) / 64);
-    kp.n_items = (S + MSA_WAVES - 1) / MSA_WAVES;
+    kp.n_items = (S + W - 1) / W;
   } else {
     kp.n_items = (int)desc->n_pairs;
   }
-  const size_t lds_ints = 16 + (size_t)kp.sched_cap * 8 + (size_t)(2 * MSA_WAVES + 1) * P->nc * MSA_RING +
+  const size_t lds_ints = 16 + (size_t)kp.sched_cap * 8 + (size_t)(2 * W + 1) * P->nc * MSA_RING +
                           (size_t)P->nc * kp.lds_row_words + (size_t)kp.lds_code_bytes;  // 4 copies = bytes*4/4
   P->lds_bytes = lds_ints * 4;
   if (P->lds_bytes > 160 * 1024) {
@@ -275,7 +288,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     return MSA_ERR_HIP;
   }
   int occ = 1;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)P->fn, MSA_THREADS, P->lds_bytes) != hipSuccess || occ < 1)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)P->fn, (W + 1) * 64, P->lds_bytes) != hipSuccess || occ < 1)
     occ = 1;
   hipDeviceProp_t prop;
   int dev = 0;
@@ -353,7 +366,7 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
   a.stamps = P->stamps;
   HIPCHK(hipMemsetAsync(P->d_ticket, 0, 64, st));
   HIPCHK(hipEventRecord(P->ev0, st));
-  hipLaunchKernelGGL(P->fn, dim3(P->grid), dim3(MSA_THREADS), P->lds_bytes, st, a);
+  hipLaunchKernelGGL(P->fn, dim3(P->grid), dim3((P->W + 1) * 64), P->lds_bytes, st, a);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(P->ev1, st));
   const int sw = (P->kp.alg == MSA_ALG_SWL || P->kp.alg == MSA_ALG_SWA) ? 1 : 0;

@@ -17,8 +17,10 @@
 //    `old` operand), lane 63 hands its bottom row to the next stripe through
 //    an LDS ring (same workgroup) or 8-byte {tag,value} granules in HBM
 //    (next workgroup; tag = launch epoch, so the data is its own flag).
-//  * 8 waves per workgroup run 8 stripes in lock-step phases of 16 steps
-//    (one s_barrier per phase); stripe k starts D_k ~ 5 phases after k-1.
+//  * W compute waves per workgroup (4 = one per SIMD for a single pair, 8 in
+//    batch mode) run W stripes in lock-step phases of 16 steps (one
+//    s_barrier per phase); stripe k starts D_k ~ 5 phases after k-1.  A
+//    separate loader wave stages the row above the workgroup's first stripe.
 //  * The substitution score comes from a per-lane 8-byte profile selected by
 //    v_perm_b32 with 4 column codes at a time; the byte is sign-extended into
 //    the diagonal add by SDWA (no separate extract).
@@ -28,10 +30,10 @@
 //    = ((s * pmax*4 + t/4) * 64 + r) * 4 + t%4   <->   cell (64s+r+1, cs_s+t-r).
 //
 // Two launch modes share the kernel:
-//  * single: one pair, items = groups of 8 stripes, tickets in order
+//  * single: one pair, items = groups of W stripes, tickets in order
 //    (a workgroup only ever waits on an earlier ticket -> no deadlock).
-//  * batch: items = whole pairs; wave w runs stripes w, w+8, ...; the
-//    wave 7 -> wave 0 wrap link goes through a full LDS row buffer.
+//  * batch: items = whole pairs; wave w runs stripes w, w+W, ...; the
+//    wave W-1 -> wave 0 wrap link goes through a full LDS row buffer.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -39,13 +41,15 @@
 
 #include "msa_types.h"
 
-#define MSA_WAVES 8
+#define MSA_WAVES_SINGLE 4  // single pair: one compute wave per SIMD (latency-bound wavefront)
+#define MSA_WAVES_BATCH 8   // batch: two per SIMD (throughput-bound, hides the step chain)
 #define MSA_K 16
 #define MSA_RING 256
-#define MSA_THREADS ((MSA_WAVES + 1) * 64)
 #define MSA_ROWOFF 128
 #define MSA_GOFF 128
 #define MSA_NEG (-(1 << 30))
+#define MSA_VIRT_CODE 7u     // SW: column code outside [1, n] (real symbols use codes 0..6)
+#define MSA_VIRT_SCORE (-100)  // its profile byte (s + 2g space for SWL; < 0 is all that matters)
 
 namespace msa {
 
@@ -120,7 +124,11 @@ struct KArgs {
 template <int ALG>
 __device__ __forceinline__ void border_top(const msa_kparams& kp, int c, int (&v)[3]) {
   // Row 0 of the DP at column c (c may be < 0: unused, return NEG).
-  if constexpr (ALG == MSA_ALG_SWL || ALG == MSA_ALG_SWA) {
+  if constexpr (ALG == MSA_ALG_SWL) {
+    v[0] = c >= 0 ? kp.gap_open * c : MSA_NEG;  // G(0,c) = H(0,c) + g*c = g*c
+    v[1] = MSA_NEG;
+    v[2] = MSA_NEG;
+  } else if constexpr (ALG == MSA_ALG_SWA) {
     v[0] = c >= 0 ? 0 : MSA_NEG;  // H
     v[1] = MSA_NEG;               // F
     v[2] = MSA_NEG;
@@ -155,7 +163,11 @@ __device__ __forceinline__ void border_top(const msa_kparams& kp, int c, int (&v
 template <int ALG>
 __device__ __forceinline__ void border_left(const msa_kparams& kp, int i, int (&v)[3]) {
   // Column 0 of row i (i >= 1), state order of each algorithm.
-  if constexpr (ALG == MSA_ALG_SWL || ALG == MSA_ALG_SWA) {
+  if constexpr (ALG == MSA_ALG_SWL) {
+    v[0] = kp.gap_open * i;  // G(i,0) = H(i,0) + g*i
+    v[1] = MSA_NEG;
+    v[2] = MSA_NEG;
+  } else if constexpr (ALG == MSA_ALG_SWA) {
     v[0] = 0;        // H
     v[1] = MSA_NEG;  // E
     v[2] = MSA_NEG;  // F
@@ -195,16 +207,25 @@ struct LaneState {
 
 // One DP step for every lane.  in[v] = value lane 0 takes from the row above.
 // Returns the direction byte for O_DIR.
+//
+// SW linear runs in shifted space G(i,j) = H(i,j) + g*(i+j):
+//   G = max(G(i-1,j-1) + s + 2g,  G(i-1,j),  G(i,j-1),  g*(i+j))
+// (the 2g is folded into the substitution profile), so the loop-carried chain
+// per step is DPP -> v_max3 instead of DPP -> max -> sub -> max3.  Rings and
+// granules carry G; H = G - g*(i+j) is only formed for the output / best.
 template <int ALG, int OUT, bool MASKED, bool TRACKPOS>
 __device__ __forceinline__ unsigned step(const msa_kparams& kp, LaneState<ALG>& L, const int (&in)[3], int s,
-                                         int t, int (&carry)[3]) {
+                                         int t, int ct, int (&carry)[3], int& hout) {
   unsigned dir = 0;
   int nS[3];
   if constexpr (ALG == MSA_ALG_SWL) {
+    // ct = g*(i+j) is the same for every lane (one anti-diagonal): an SGPR
     const int up = dpp_shr1(in[0], L.S[0]);
-    const int d = L.U[0] + s;
-    const int e = imax(up, L.S[0]) - kp.gap_open;
-    nS[0] = imax3(d, e, 0);
+    const int x = imax(L.U[0] + s, ct);
+    nS[0] = imax3(x, up, L.S[0]);
+    // opaque: keeps G a real per-step value (otherwise LLVM flattens the
+    // running max3 chain and distributes the "- ct" over every term)
+    asm("" : "+v"(nS[0]));
     L.U[0] = up;
   } else if constexpr (ALG == MSA_ALG_SWA) {
     const int upH = dpp_shr1(in[0], L.S[0]);
@@ -274,11 +295,13 @@ __device__ __forceinline__ unsigned step(const msa_kparams& kp, LaneState<ALG>& 
 #pragma unroll
     for (int v = 0; v < NS; ++v) nS[v] = before ? L.LB[v] : (after ? MSA_NEG : nS[v]);
     if constexpr (ALG == MSA_ALG_SWL || ALG == MSA_ALG_SWA) {
+      const int hv = (ALG == MSA_ALG_SWL) ? nS[0] - ct : nS[0];
+      hout = hv;
       if (!before && !after) {
         if constexpr (TRACKPOS) {
-          if (nS[0] > L.best) { L.best = nS[0]; L.bt = t; }
+          if (hv > L.best) { L.best = hv; L.bt = t; }
         } else {
-          L.best = imax(L.best, nS[0]);
+          L.best = imax(L.best, hv);
         }
       }
     } else {
@@ -289,10 +312,12 @@ __device__ __forceinline__ unsigned step(const msa_kparams& kp, LaneState<ALG>& 
     }
   } else {
     if constexpr (ALG == MSA_ALG_SWL || ALG == MSA_ALG_SWA) {
+      const int hv = (ALG == MSA_ALG_SWL) ? nS[0] - ct : nS[0];
+      hout = hv;
       if constexpr (TRACKPOS) {
-        if (nS[0] > L.best) { L.best = nS[0]; L.bt = t; }
+        if (hv > L.best) { L.best = hv; L.bt = t; }
       } else {
-        L.best = imax(L.best, nS[0]);
+        L.best = imax(L.best, hv);
       }
     }
   }
@@ -323,7 +348,7 @@ __device__ __forceinline__ void gstore(unsigned long long* p, unsigned long long
 enum Src { SRC_BORDER = 0, SRC_RING = 1, SRC_ROW = 2, SRC_GLOBAL = 3 };
 enum Snk { SNK_NONE = 0, SNK_RING = 1, SNK_ROW = 2, SNK_GLOBAL = 3 };
 
-// Loader wave (wave MSA_WAVES): in single mode it pulls the row above the
+// Loader wave (wave W): in single mode it pulls the row above the
 // item's first stripe from the previous workgroup's granules (HBM, `sc1`)
 // into the LDS staging ring MSA_LOAD_AHEAD phases ahead, so no compute wave
 // ever waits on a global load.  Prefetch slots are compile-time indices
@@ -351,7 +376,7 @@ __device__ __forceinline__ void loader_commit(const KArgs& a, const StripeGeom& 
       break;
     }
   }
-  if (v < NC) stage[v * MSA_RING + ((16 * q + l) & (MSA_RING - 1))] = (int)(unsigned)gv;
+  if (v < NC) stage[v * MSA_RING + ((16 * q + l) & (MSA_RING - 1))] = need ? (int)(unsigned)gv : MSA_NEG;
 }
 
 template <int NC>
@@ -362,10 +387,13 @@ __device__ __forceinline__ unsigned long long loader_issue(const KArgs& a, const
   return gload(g_in + (size_t)v * a.gbuf_stride + col + MSA_GOFF);
 }
 
-template <int ALG, int OUT, bool TRACKPOS>
-__global__ __launch_bounds__(MSA_THREADS) void stripe_kernel(KArgs a) {
+template <int ALG, int OUT, bool TRACKPOS, int W>
+__global__ __launch_bounds__((W + 1) * 64) void stripe_kernel(KArgs a) {
   constexpr int NC = Tr<ALG>::NC;
-  constexpr int W = MSA_WAVES;
+  // Smith-Waterman kernels never mask: columns outside [1, n] carry the
+  // virtual code whose score (MSA_VIRT_SCORE) keeps every out-of-matrix cell
+  // strictly below a real cell, so the plain recurrence runs over them.
+  constexpr bool SWK = (ALG == MSA_ALG_SWL || ALG == MSA_ALG_SWA);
   constexpr int LA = MSA_LOAD_AHEAD;
   extern __shared__ __attribute__((aligned(16))) int smem[];
   const msa_kparams& kp = a.kp;
@@ -452,7 +480,7 @@ __global__ __launch_bounds__(MSA_THREADS) void stripe_kernel(KArgs a) {
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
           const int col = cbase + 4 * d + cp + b;
-          const unsigned code = (col >= 1 && col <= n) ? (unsigned)Bp[col - 1] : 0u;
+          const unsigned code = (col >= 1 && col <= n) ? (unsigned)Bp[col - 1] : (SWK ? MSA_VIRT_CODE : 0u);
           word |= (code & 7u) << (8 * b);
         }
         codes[cp * code_dwords + d] = word;
@@ -523,271 +551,279 @@ __global__ __launch_bounds__(MSA_THREADS) void stripe_kernel(KArgs a) {
     }
 
     // =================== compute waves ===================
-    LaneState<ALG> L;
-    int cur = w;
-    StripeGeom sg;
-    int snk = SNK_NONE;
-    int out_cs = 0;   // consumer cs (for output indexing)
-    int out_chi = 0;  // producer c_hi seen by the consumer (input masking)
-    int* ring_out = nullptr;
-    const int* in_ptr = nullptr;  // LDS input rows: in_ptr + v*in_vs + ((16q + 4u) & in_mask)
-    int in_vs = MSA_RING, in_mask = MSA_RING - 1;
-    int* out_ptr = nullptr;       // LDS output rows: out_ptr + v*out_vs + ((x + out_add) & out_mask)
-    int out_vs = MSA_RING, out_mask = MSA_RING - 1, out_add = 0, out_lim = 1 << 30;
-    unsigned long long* g_out = nullptr;
-    size_t obase = 0;  // element (O_H/O_TAB) or byte (O_DIR) base of this stripe in the output
+    // Wave w runs stripes w, w+W, ...  Every wave passes exactly `total`
+    // barriers (one per phase): idle phases before a stripe's start T, then
+    // the stripe's P phases as three loops -- masked head, unmasked body (no
+    // per-step range checks, no per-phase bookkeeping), masked tail.
     __syncthreads();  // pairs with the loader's post-staging barrier
-
-    for (int ph = 0; ph < total; ++ph) {
-#ifdef MSA_STAMPS
-      if (a.stamps && item == 0 && w == 2 && ph < 4096) {
-        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-        if (lane == 0) a.stamps[3 * ph] = t0;
+    int ph = 0;
+    for (int cur = w; cur < ns; cur += W) {
+      StripeGeom sg = sched[cur];
+      sg.T = uni(sg.T); sg.P = uni(sg.P); sg.cs = uni(sg.cs); sg.lead = uni(sg.lead);
+      sg.mask_lo = uni(sg.mask_lo); sg.mask_hi = uni(sg.mask_hi); sg.c_hi = uni(sg.c_hi);
+      for (; ph < sg.T; ++ph) __syncthreads();
+      // ---- stripe init ----
+      const int ks = k0 + cur;  // pair-local stripe index
+      LaneState<ALG> L;
+      L.i = 64 * ks + lane + 1;
+      const int ivalid = min(L.i, m);
+      L.tmin = jlo_of(L.i, kp.band) - sg.cs + lane;
+      L.tmax = (L.i <= m) ? jhi_of(L.i, n, kp.band) - sg.cs + lane : -1;
+      {
+        int lb[3];
+        border_left<ALG>(kp, ivalid, lb);
+        if (kp.band >= 0 && jlo_of(L.i, kp.band) > 1) lb[0] = lb[1] = lb[2] = MSA_NEG;
+#pragma unroll
+        for (int v = 0; v < 3; ++v) { L.LB[v] = lb[v]; L.S[v] = lb[v]; L.U[v] = MSA_NEG; L.fin[v] = 0; }
       }
-#endif
-      if (cur < ns) {
-        const int Tc = uni(sched[cur].T);
-        if (ph == Tc) {
-          // ---- stripe init ----
-          sg = sched[cur];
-          sg.T = uni(sg.T); sg.P = uni(sg.P); sg.cs = uni(sg.cs); sg.lead = uni(sg.lead);
-          sg.mask_lo = uni(sg.mask_lo); sg.mask_hi = uni(sg.mask_hi); sg.c_hi = uni(sg.c_hi);
-          const int ks = k0 + cur;  // pair-local stripe index
-          L.i = 64 * ks + lane + 1;
-          const int ivalid = min(L.i, m);
-          L.tmin = jlo_of(L.i, kp.band) - sg.cs + lane;
-          L.tmax = (L.i <= m) ? jhi_of(L.i, n, kp.band) - sg.cs + lane : -1;
-          int lb[3];
-          border_left<ALG>(kp, ivalid, lb);
-          if (kp.band >= 0 && jlo_of(L.i, kp.band) > 1) lb[0] = lb[1] = lb[2] = MSA_NEG;
+      L.best = 0;
+      L.bt = -1;
+      const int gdiag = kp.gap_open * (64 * ks + 1 + sg.cs);  // SWL: g*(i+j) at step 0, same for all lanes
+      // SWL: the lane starts left of the matrix on virtual cells with H = 0,
+      // i.e. G = g*(i+j); its left neighbour at step 0 is G = gdiag - g
+      if constexpr (ALG == MSA_ALG_SWL) L.S[0] = gdiag - kp.gap_open;
+      // substitution profile of this row (codes 0..7)
+      {
+        const unsigned ac = (L.i <= m) ? (a.A[pd.a_off + L.i - 1] & 7u) : 0u;
+        int sm, sx;
+        if constexpr (ALG == MSA_ALG_REF || ALG == MSA_ALG_NWA) { sm = 1; sx = 0; }
+        else if constexpr (ALG == MSA_ALG_PART) { sm = 0; sx = 1; }
+        else if constexpr (ALG == MSA_ALG_SWL) { sm = kp.match + 2 * kp.gap_open; sx = kp.mismatch + 2 * kp.gap_open; }
+        else { sm = kp.match; sx = kp.mismatch; }
+        const unsigned bx = (unsigned)(sx & 0xff) * 0x01010101u;
+        unsigned lo = bx, hi = bx;
+        const unsigned bm = (unsigned)(sm & 0xff);
+        if (ac < 4) lo = (lo & ~(0xffu << (8 * ac))) | (bm << (8 * ac));
+        else hi = (hi & ~(0xffu << (8 * (ac - 4)))) | (bm << (8 * (ac - 4)));
+        if constexpr (SWK) hi = (hi & 0x00ffffffu) | ((unsigned)(MSA_VIRT_SCORE & 0xff) << 24);
+        L.plo = lo;
+        L.phi = hi;
+      }
+      // code stream: lane reads bytes starting at column cs - lane
+      {
+        const int b0 = sg.cs - lane - cbase;  // >= 1 by construction
+        L.cw_copy = b0 & 3;
+        L.cw_base = L.cw_copy * code_dwords + (b0 >> 2);
+      }
+      // input: the loader's staging ring (row 0 or the previous workgroup),
+      // the wrap row buffer (batch), or the ring of the previous wave
+      const int* in_ptr;
+      int in_vs, in_mask;
+      const int par_in = ((cur - 1) / W) & 1;  // round parity of the producer stripe
+      if (cur == 0) {
+        in_ptr = stage; in_vs = MSA_RING; in_mask = MSA_RING - 1;
+      } else if (cur % W == 0) {
+        in_ptr = rowbuf + MSA_ROWOFF; in_vs = kp.lds_row_words; in_mask = 0x3fffffff;
+      } else {
+        in_ptr = rings + ((par_in * W + (w - 1)) * NC) * MSA_RING; in_vs = MSA_RING; in_mask = MSA_RING - 1;
+      }
+      int snk;
+      if (cur == ns - 1) snk = (kp.single && ks < S_pair - 1) ? SNK_GLOBAL : SNK_NONE;
+      else snk = (cur % W == W - 1) ? SNK_ROW : SNK_RING;
+      int* const ring_out = rings + (((cur / W) & 1) * W + w) * NC * MSA_RING;
+      int* out_ptr;
+      int out_vs, out_mask, out_add, out_lim;
+      if (snk == SNK_ROW) {
+        out_ptr = rowbuf; out_vs = kp.lds_row_words; out_mask = 0x3fffffff; out_add = MSA_ROWOFF;
+        out_lim = kp.lds_row_words - 4;
+      } else {
+        out_ptr = ring_out; out_vs = MSA_RING; out_mask = MSA_RING - 1; out_add = 0; out_lim = 1 << 30;
+      }
+      int out_cs = 0;
+      if (snk != SNK_NONE) {
+        StripeGeom gn;
+        stripe_geom(ks + 1, m, n, kp.band, gn);
+        out_cs = gn.cs;
+      }
+      int out_chi = n;  // c_hi of the producer row above (input masking, banded)
+      if (ks > 0) {
+        StripeGeom gp;
+        stripe_geom(ks - 1, m, n, kp.band, gp);
+        out_chi = gp.c_hi;
+      }
+      snk = uni(snk); out_cs = uni(out_cs); out_chi = uni(out_chi);
+      unsigned long long* const g_out = (snk == SNK_GLOBAL) ? a.gbuf + (size_t)group * NC * a.gbuf_stride : nullptr;
+      const size_t obase = (size_t)pd.out_off + (size_t)ks * pd.pmax * MSA_K * 64;
+
+      auto run_phase = [&](const int q, auto MASKED_, auto INMASK_) {
+        constexpr bool MASKED = decltype(MASKED_)::value;  // per-lane start/end checks
+        constexpr bool INMASK = decltype(INMASK_)::value;  // input columns beyond the producer's last
+
+        // ---- all LDS reads of the phase up front (one exposed latency per phase) ----
+        int IN[NC][16];
+        {
+          const int* base = in_ptr + ((16 * q) & in_mask);
 #pragma unroll
-          for (int v = 0; v < 3; ++v) { L.LB[v] = lb[v]; L.S[v] = lb[v]; L.U[v] = MSA_NEG; L.fin[v] = 0; }
-          L.best = 0;
-          L.bt = -1;
-          // substitution profile of this row (codes 0..7)
-          {
-            const unsigned ac = (L.i <= m) ? (a.A[pd.a_off + L.i - 1] & 7u) : 0u;
-            int sm, sx;
-            if constexpr (ALG == MSA_ALG_REF || ALG == MSA_ALG_NWA) { sm = 1; sx = 0; }
-            else if constexpr (ALG == MSA_ALG_PART) { sm = 0; sx = 1; }
-            else { sm = kp.match; sx = kp.mismatch; }
-            const unsigned bx = (unsigned)(sx & 0xff) * 0x01010101u;
-            unsigned lo = bx, hi = bx;
-            const unsigned bm = (unsigned)(sm & 0xff);
-            if (ac < 4) lo = (lo & ~(0xffu << (8 * ac))) | (bm << (8 * ac));
-            else hi = (hi & ~(0xffu << (8 * (ac - 4)))) | (bm << (8 * (ac - 4)));
-            L.plo = lo;
-            L.phi = hi;
-          }
-          // code stream: lane reads bytes starting at column cs - lane
-          {
-            const int b0 = sg.cs - lane - cbase;  // >= 1 by construction
-            L.cw_copy = b0 & 3;
-            L.cw_base = L.cw_copy * code_dwords + (b0 >> 2);
-          }
-          // input source: border row, ring of the previous wave (same round
-          // parity), the wrap row buffer, or the loader's staging ring
-          const int par_in = ((cur - 1) / W) & 1;  // round parity of the producer stripe
-          if (cur == 0) {
-            in_ptr = stage; in_vs = MSA_RING; in_mask = MSA_RING - 1;  // loader: row 0 or the previous group
-          } else if (cur % W == 0) {
-            in_ptr = rowbuf + MSA_ROWOFF; in_vs = kp.lds_row_words; in_mask = 0x3fffffff;
-          } else {
-            in_ptr = rings + ((par_in * W + (w - 1)) * NC) * MSA_RING; in_vs = MSA_RING; in_mask = MSA_RING - 1;
-          }
-          if (cur == ns - 1) {
-            snk = (kp.single && ks < S_pair - 1) ? SNK_GLOBAL : SNK_NONE;
-          } else {
-            snk = (cur % W == W - 1) ? SNK_ROW : SNK_RING;
-          }
-          ring_out = rings + (((cur / W) & 1) * W + w) * NC * MSA_RING;
-          if (snk == SNK_ROW) {
-            out_ptr = rowbuf; out_vs = kp.lds_row_words; out_mask = 0x3fffffff; out_add = MSA_ROWOFF;
-            out_lim = kp.lds_row_words - 4;
-          } else {
-            out_ptr = ring_out; out_vs = MSA_RING; out_mask = MSA_RING - 1; out_add = 0; out_lim = 1 << 30;
-          }
-          if (snk != SNK_NONE) {
-            StripeGeom gn;
-            stripe_geom(ks + 1, m, n, kp.band, gn);
-            out_cs = gn.cs;
-          }
-          if (ks > 0) {
-            StripeGeom gp;
-            stripe_geom(ks - 1, m, n, kp.band, gp);
-            out_chi = gp.c_hi;  // c_hi of the producer row above (input masking, banded)
-          } else {
-            out_chi = n;
-          }
-          g_out = (snk == SNK_GLOBAL) ? a.gbuf + (size_t)group * NC * a.gbuf_stride : nullptr;
-          obase = (size_t)pd.out_off + (size_t)ks * pd.pmax * MSA_K * 64;
-        }
-        if (ph >= Tc) {
-          const int q = ph - Tc;
-          const bool masked = uni((16 * q < sg.mask_lo) || (16 * q + 15 > sg.mask_hi));
-          const bool inmask = uni(sg.cs + 16 * q + 15 > out_chi);
-          auto run_phase = [&](auto MASKED_, auto INMASK_) {
-            constexpr bool MASKED = decltype(MASKED_)::value;
-            constexpr bool INMASK = decltype(INMASK_)::value;
-            // ---- all LDS reads of the phase up front (one exposed latency per phase) ----
-            int IN[NC][16];
-            {
-              const int* base = in_ptr + ((16 * q) & in_mask);
-#pragma unroll
-              for (int v = 0; v < NC; ++v) {
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                  const int4 x = *reinterpret_cast<const int4*>(base + v * in_vs + 4 * u);
-                  IN[v][4 * u + 0] = x.x; IN[v][4 * u + 1] = x.y; IN[v][4 * u + 2] = x.z; IN[v][4 * u + 3] = x.w;
-                }
-              }
-              if constexpr (INMASK) {
-#pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                  const bool o = sg.cs + 16 * q + k > out_chi;
-#pragma unroll
-                  for (int v = 0; v < NC; ++v) IN[v][k] = o ? MSA_NEG : IN[v][k];
-                }
-              }
-            }
-            unsigned cw[4];
-            {
-              const unsigned* cp = codes + L.cw_base + 4 * q;
-              cw[0] = cp[0]; cw[1] = cp[1]; cw[2] = cp[2]; cw[3] = cp[3];
-            }
-            int hist[NC][16];
-            unsigned dirw[4] = {0u, 0u, 0u, 0u};
-            int4* hrow = reinterpret_cast<int4*>(a.outH + obase) + (size_t)(4 * q) * 64 + lane;
-            int4* t2row = reinterpret_cast<int4*>(a.outT2 + obase) + (size_t)(4 * q) * 64 + lane;
-            int4* t3row = reinterpret_cast<int4*>(a.outT3 + obase) + (size_t)(4 * q) * 64 + lane;
+          for (int v = 0; v < NC; ++v) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-              const unsigned s4 = __builtin_amdgcn_perm(L.phi, L.plo, cw[u]);
-              unsigned dq = 0;
-#pragma unroll
-              for (int kk = 0; kk < 4; ++kk) {
-                const int k = 4 * u + kk;
-                const int t = 16 * q + k;
-                const int s = ((int)(s4 << (24 - 8 * kk))) >> 24;
-                int inv[3];
-#pragma unroll
-                for (int v = 0; v < NC; ++v) inv[v] = IN[v][k];
-                int cr[3];
-                const unsigned d = step<ALG, OUT, MASKED, TRACKPOS>(kp, L, inv, s, t, cr);
-#pragma unroll
-                for (int v = 0; v < NC; ++v) hist[v][k] = cr[v];
-                dq |= d << (8 * kk);
-              }
-              dirw[u] = dq;
-              // cell outputs: one 1 KiB coalesced store per wave per 4 steps
-              if constexpr (OUT == MSA_OUT_H) {
-                int4 hv;
-                if constexpr (ALG == MSA_ALG_REF || ALG == MSA_ALG_PART) {
-                  hv = make_int4(imax3(hist[0][4 * u], hist[1][4 * u], hist[2][4 * u]),
-                                 imax3(hist[0][4 * u + 1], hist[1][4 * u + 1], hist[2][4 * u + 1]),
-                                 imax3(hist[0][4 * u + 2], hist[1][4 * u + 2], hist[2][4 * u + 2]),
-                                 imax3(hist[0][4 * u + 3], hist[1][4 * u + 3], hist[2][4 * u + 3]));
-                } else {
-                  hv = make_int4(hist[0][4 * u], hist[0][4 * u + 1], hist[0][4 * u + 2], hist[0][4 * u + 3]);
-                }
-                hrow[u * 64] = hv;
-              } else if constexpr (OUT == MSA_OUT_TAB) {
-                hrow[u * 64] = make_int4(hist[0][4 * u], hist[0][4 * u + 1], hist[0][4 * u + 2], hist[0][4 * u + 3]);
-                t2row[u * 64] = make_int4(hist[1][4 * u], hist[1][4 * u + 1], hist[1][4 * u + 2], hist[1][4 * u + 3]);
-                t3row[u * 64] = make_int4(hist[2][4 * u], hist[2][4 * u + 1], hist[2][4 * u + 2], hist[2][4 * u + 3]);
-              }
+              const int4 x = *reinterpret_cast<const int4*>(base + v * in_vs + 4 * u);
+              IN[v][4 * u + 0] = x.x; IN[v][4 * u + 1] = x.y; IN[v][4 * u + 2] = x.z; IN[v][4 * u + 3] = x.w;
             }
-            if constexpr (OUT == MSA_OUT_DIR) {
-              reinterpret_cast<uint4*>(a.outDir + obase)[(size_t)q * 64 + lane] =
-                  make_uint4(dirw[0], dirw[1], dirw[2], dirw[3]);
-            }
-            // hand the bottom row to the next stripe: lane 63, once per phase
-            if (snk != SNK_NONE && lane == 63) {
-              const int x = (sg.cs + 16 * q - 63 - out_cs + out_add) & out_mask;  // multiple of 16
-              if (x >= 0 && x + 12 <= out_lim) {
-                int* dst = out_ptr + x;
-#pragma unroll
-                for (int v = 0; v < NC; ++v)
-#pragma unroll
-                  for (int u = 0; u < 4; ++u)
-                    *reinterpret_cast<int4*>(dst + v * out_vs + 4 * u) =
-                        make_int4(hist[v][4 * u], hist[v][4 * u + 1], hist[v][4 * u + 2], hist[v][4 * u + 3]);
-              }
-            }
-            // global sink: 8-byte {epoch, value} granules for the 16 columns of this phase
-            if (snk == SNK_GLOBAL) {
-              asm volatile("" ::: "memory");  // lane 63's ring writes stay ahead of these reads
-              const int v = lane >> 4, l = lane & 15;
-              if (v < NC) {
-                const int x = sg.cs + 16 * q - 63 - out_cs + l;
-                const int col = sg.cs + 16 * q - 63 + l;
-                if (col + MSA_GOFF >= 0 && col + MSA_GOFF < a.gbuf_stride) {
-                  const int val = ring_out[v * MSA_RING + (x & (MSA_RING - 1))];
-                  gstore(g_out + (size_t)v * a.gbuf_stride + col + MSA_GOFF,
-                         ((unsigned long long)ep << 32) | (unsigned)val);
-                }
-              }
-            }
-          };
-          using T_ = std::true_type;
-          using F_ = std::false_type;
-          if (inmask) {
-            if (masked) run_phase(T_{}, T_{}); else run_phase(F_{}, T_{});
-          } else {
-            if (masked) run_phase(T_{}, F_{}); else run_phase(F_{}, F_{});
           }
-          if (q == sg.P - 1) {
-            // ---- stripe finalize ----
-            const int ks = k0 + cur;
-            msa_stripe_meta* md = a.meta + pd.stripe0 + ks;
-            if constexpr (ALG == MSA_ALG_SWL || ALG == MSA_ALG_SWA) {
-              // first max in row-major order: max best, then min row
-              int b = (L.i <= m) ? L.best : INT32_MIN;
-              int bi = L.i;
-              int bj = sg.cs + L.bt - lane;
+          if constexpr (INMASK) {
 #pragma unroll
-              for (int off = 32; off >= 1; off >>= 1) {
-                const int ob = __shfl_xor(b, off);
-                const int oi = __shfl_xor(bi, off);
-                const int oj = __shfl_xor(bj, off);
-                if (ob > b || (ob == b && oi < bi)) { b = ob; bi = oi; bj = oj; }
-              }
-              if (lane == 0) {
-                md->best = b;
-                md->best_i = bi;
-                md->best_j = TRACKPOS ? bj : -1;
-              }
-            } else {
-              if (L.i == m) {
-                md->fin[0] = L.fin[0];
-                md->fin[1] = L.fin[1];
-                md->fin[2] = L.fin[2];
-                md->has_fin = 1;
-              }
+            for (int k = 0; k < 16; ++k) {
+              const bool o = sg.cs + 16 * q + k > out_chi;
+#pragma unroll
+              for (int v = 0; v < NC; ++v) IN[v][k] = o ? MSA_NEG : IN[v][k];
             }
-            if (lane == 0) {
-              md->cs = sg.cs;
-              md->phases = sg.P;
-            }
-            cur += W;
           }
         }
+        unsigned cw[4];
+        {
+          const unsigned* cp = codes + L.cw_base + 4 * q;  // per-lane, dword aligned only
+          cw[0] = cp[0]; cw[1] = cp[1]; cw[2] = cp[2]; cw[3] = cp[3];
+        }
+        int hist[NC][16];
+        int hv[16];
+        unsigned dirw[4] = {0u, 0u, 0u, 0u};
+        int4* hrow = reinterpret_cast<int4*>(a.outH + obase) + (size_t)(4 * q) * 64 + lane;
+        int4* t2row = reinterpret_cast<int4*>(a.outT2 + obase) + (size_t)(4 * q) * 64 + lane;
+        int4* t3row = reinterpret_cast<int4*>(a.outT3 + obase) + (size_t)(4 * q) * 64 + lane;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const unsigned s4 = __builtin_amdgcn_perm(L.phi, L.plo, cw[u]);
+          unsigned dq = 0;
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) {
+            const int k = 4 * u + kk;
+            const int t = 16 * q + k;
+            const int s = ((int)(s4 << (24 - 8 * kk))) >> 24;
+            int inv[3];
+#pragma unroll
+            for (int v = 0; v < NC; ++v) inv[v] = IN[v][k];
+            int cr[3];
+            int ct = gdiag + kp.gap_open * t;
+            if constexpr (ALG == MSA_ALG_SWL) asm("" : "+s"(ct));  // one SGPR feeds both the floor and H
+            const unsigned d = step<ALG, OUT, MASKED, TRACKPOS>(kp, L, inv, s, t, ct, cr, hv[k]);
+#pragma unroll
+            for (int v = 0; v < NC; ++v) hist[v][k] = cr[v];
+            dq |= d << (8 * kk);
+          }
+          dirw[u] = dq;
+          // cell outputs: one 1 KiB coalesced store per wave per 4 steps
+          if constexpr (OUT == MSA_OUT_H) {
+            int4 h4;
+            if constexpr (ALG == MSA_ALG_REF || ALG == MSA_ALG_PART) {
+              h4 = make_int4(imax3(hist[0][4 * u], hist[1][4 * u], hist[2][4 * u]),
+                             imax3(hist[0][4 * u + 1], hist[1][4 * u + 1], hist[2][4 * u + 1]),
+                             imax3(hist[0][4 * u + 2], hist[1][4 * u + 2], hist[2][4 * u + 2]),
+                             imax3(hist[0][4 * u + 3], hist[1][4 * u + 3], hist[2][4 * u + 3]));
+            } else if constexpr (ALG == MSA_ALG_SWL || ALG == MSA_ALG_SWA) {
+              h4 = make_int4(hv[4 * u], hv[4 * u + 1], hv[4 * u + 2], hv[4 * u + 3]);
+            } else {
+              h4 = make_int4(hist[0][4 * u], hist[0][4 * u + 1], hist[0][4 * u + 2], hist[0][4 * u + 3]);
+            }
+            hrow[u * 64] = h4;
+          } else if constexpr (OUT == MSA_OUT_TAB) {
+            hrow[u * 64] = make_int4(hist[0][4 * u], hist[0][4 * u + 1], hist[0][4 * u + 2], hist[0][4 * u + 3]);
+            t2row[u * 64] = make_int4(hist[1][4 * u], hist[1][4 * u + 1], hist[1][4 * u + 2], hist[1][4 * u + 3]);
+            t3row[u * 64] = make_int4(hist[2][4 * u], hist[2][4 * u + 1], hist[2][4 * u + 2], hist[2][4 * u + 3]);
+          }
+        }
+        if constexpr (OUT == MSA_OUT_DIR) {
+          reinterpret_cast<uint4*>(a.outDir + obase)[(size_t)q * 64 + lane] =
+              make_uint4(dirw[0], dirw[1], dirw[2], dirw[3]);
+        }
+        // hand the bottom row to the next stripe: lane 63, once per phase
+        if (snk != SNK_NONE && lane == 63) {
+          const int x = (sg.cs + 16 * q - 63 - out_cs + out_add) & out_mask;  // multiple of 16
+          if (x >= 0 && x + 12 <= out_lim) {
+            int* dst = out_ptr + x;
+#pragma unroll
+            for (int v = 0; v < NC; ++v)
+#pragma unroll
+              for (int u = 0; u < 4; ++u)
+                *reinterpret_cast<int4*>(dst + v * out_vs + 4 * u) =
+                    make_int4(hist[v][4 * u], hist[v][4 * u + 1], hist[v][4 * u + 2], hist[v][4 * u + 3]);
+          }
+        }
+        // global sink: 8-byte {epoch, value} granules for the 16 columns of this phase
+        if (snk == SNK_GLOBAL) {
+          asm volatile("" ::: "memory");  // lane 63's ring writes stay ahead of these reads
+          const int v = lane >> 4, l = lane & 15;
+          if (v < NC) {
+            const int x = sg.cs + 16 * q - 63 - out_cs + l;
+            const int col = sg.cs + 16 * q - 63 + l;
+            if (col + MSA_GOFF >= 0 && col + MSA_GOFF < a.gbuf_stride) {
+              const int val = ring_out[v * MSA_RING + (x & (MSA_RING - 1))];
+              gstore(g_out + (size_t)v * a.gbuf_stride + col + MSA_GOFF, ((unsigned long long)ep << 32) | (unsigned)val);
+            }
+          }
+        }
+      };
+      using T_ = std::true_type;
+      using F_ = std::false_type;
+      // phase q needs no range checks iff 16q >= mask_lo (every lane has
+      // started), 16q+15 <= mask_hi (none has finished) and every input column
+      // cs+16q+15 <= out_chi
+      const int P = sg.P;
+      const int lim = min(sg.mask_hi, out_chi - sg.cs) - 15;
+      const int qa = uni(min(P, sg.mask_lo <= 0 ? 0 : (sg.mask_lo + 15) / 16));
+      const int qb = uni(max(qa, min(P, lim >= 0 ? lim / 16 + 1 : 0)));
+      int q = 0;
+      if constexpr (SWK) {
+        // no state masking; only the inputs past the producer's last column
+        // (never written into the ring / granules) are replaced by -inf
+        const int li = out_chi - sg.cs - 15;
+        const int qi = uni(min(P, li >= 0 ? li / 16 + 1 : 0));
+        for (; q < qi; ++q) {
+          run_phase(q, F_{}, F_{});
+          __syncthreads();
+        }
+        for (; q < P; ++q) {
+          run_phase(q, F_{}, T_{});
+          __syncthreads();
+        }
+      } else {
+        for (; q < qa; ++q) {
+          run_phase(q, T_{}, T_{});
+          __syncthreads();
+        }
+        for (; q < qb; ++q) {
+          run_phase(q, F_{}, F_{});
+          __syncthreads();
+        }
+        for (; q < P; ++q) {
+          run_phase(q, T_{}, T_{});
+          __syncthreads();
+        }
       }
-#ifdef MSA_STAMPS
-      if (a.stamps && item == 0 && w == 2 && ph < 4096) {
-        __builtin_amdgcn_s_waitcnt(0);
-        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-        if (lane == 0) a.stamps[3 * ph + 1] = t1;
+      ph += P;
+      // ---- stripe finalize ----
+      msa_stripe_meta* md = a.meta + pd.stripe0 + ks;
+      if constexpr (ALG == MSA_ALG_SWL || ALG == MSA_ALG_SWA) {
+        // first max in row-major order: max best, then min row
+        int b = (L.i <= m) ? L.best : INT32_MIN;
+        int bi = L.i;
+        int bj = sg.cs + L.bt - lane;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+          const int ob = __shfl_xor(b, off);
+          const int oi = __shfl_xor(bi, off);
+          const int oj = __shfl_xor(bj, off);
+          if (ob > b || (ob == b && oi < bi)) { b = ob; bi = oi; bj = oj; }
+        }
+        if (lane == 0) {
+          md->best = b;
+          md->best_i = bi;
+          md->best_j = TRACKPOS ? bj : -1;
+        }
+      } else {
+        if (L.i == m) {
+          md->fin[0] = L.fin[0];
+          md->fin[1] = L.fin[1];
+          md->fin[2] = L.fin[2];
+          md->has_fin = 1;
+        }
       }
-#endif
-      __syncthreads();
-#ifdef MSA_STAMPS
-      if (a.stamps && item == 0 && w == 2 && ph < 4096) {
-        const unsigned long long t2 = __builtin_amdgcn_s_memtime();
-        if (lane == 0) a.stamps[3 * ph + 2] = t2;
+      if (lane == 0) {
+        md->cs = sg.cs;
+        md->phases = sg.P;
       }
-#endif
     }
+    for (; ph < total; ++ph) __syncthreads();
   }
 }
 

@@ -98,7 +98,9 @@ int msa_partial_tables(const char* A0, const char* B0, size_t m, size_t n, doubl
  * A plan owns the device scratch for one shape of work; running it launches
  * the stripe kernel + a tiny per-pair reduction on `stream` (no allocation,
  * no host sync inside msa_plan_run).  Inputs are uint8 codes in [0,8) already
- * in device memory (see msa_encode_pair for the host-side code map). */
+ * in device memory (see msa_encode_pair for the host-side code map); the
+ * Smith-Waterman algorithms reserve code 7 (out-of-matrix sentinel), so their
+ * inputs use codes 0..6. */
 typedef enum msa_alg_e {
   MSA_SW_LINEAR = 0,  /* Smith-Waterman, linear gap (gap_open == gap_extend used) */
   MSA_SW_AFFINE = 1,  /* Smith-Waterman, affine gap */
@@ -161,7 +163,8 @@ int msa_encode_pair(const char* A0, size_t m, const char* B0, size_t n, uint8_t*
 
 /* Host-pointer Smith-Waterman (build extension): score, end cell (first max
  * in row-major order) and, when cigar != NULL, the traceback as a run-length
- * M/I/D string (I consumes A, D consumes B) with its start cell. */
+ * M/I/D string (I consumes A, D consumes B) with its start cell.  At most 7
+ * distinct symbols (MSA_ERR_ALPHABET otherwise). */
 int msa_sw_align(const char* A0, size_t m, const char* B0, size_t n, int32_t match, int32_t mismatch,
                  int32_t gap_open, int32_t gap_extend, int32_t* score, int64_t* end_i, int64_t* end_j,
                  int64_t* beg_i, int64_t* beg_j, char* cigar, size_t cigar_cap);

@@ -1,0 +1,51 @@
+"""Summarise a scripts/prof.sh output directory into profiles/ (committed evidence).
+
+    python scripts/pmc_summary.py gpurun_out/prof_c2 c2 r01
+
+Writes profiles/<round>_<wl>_kernel_stats.csv (rocprofv3 --stats summary),
+profiles/<round>_<wl>_pmc.json: per-launch averages of the SQ counters of the
+stripe kernel and its HBM traffic: FETCH_SIZE (doubled: on gfx950 it reports
+half the bytes of wide coalesced reads, MI355X_MICROARCH.md "HBM") + WRITE_SIZE,
+both in KB as rocprofv3 reports them, converted to bytes per launch.
+"""
+import csv
+import json
+import shutil
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+src, wl, rnd = Path(sys.argv[1]), sys.argv[2], sys.argv[3]
+dst = Path(__file__).resolve().parent.parent / "profiles"
+dst.mkdir(exist_ok=True)
+
+
+def per_dispatch(sub):
+    f = src / sub / "run_counter_collection.csv"
+    if not f.exists():
+        return {}
+    acc = defaultdict(lambda: defaultdict(float))
+    for r in csv.DictReader(open(f)):
+        if "stripe_kernel" not in r["Kernel_Name"]:
+            continue
+        acc[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
+    return {k: sum(v.values()) / len(v) for k, v in acc.items()}
+
+
+out = {"workload": wl, "round": rnd, "kernel": "stripe_kernel", "per_launch": {}}
+for sub in ("pmc1", "pmc2", "pmc_fetch", "pmc_write"):
+    out["per_launch"].update(per_dispatch(sub))
+pl = out["per_launch"]
+if "FETCH_SIZE" in pl or "WRITE_SIZE" in pl:
+    fetch = 2.0 * pl.get("FETCH_SIZE", 0.0) * 1024.0
+    write = pl.get("WRITE_SIZE", 0.0) * 1024.0
+    out["hbm_bytes_per_launch"] = {"fetch_corrected": fetch, "write": write, "total": fetch + write}
+stats = src / "trace" / "run_kernel_stats.csv"
+if stats.exists():
+    shutil.copy(stats, dst / f"{rnd}_{wl}_kernel_stats.csv")
+    for r in csv.DictReader(open(stats)):
+        if "stripe_kernel" in r["Name"]:
+            out["trace_avg_ns"] = float(r["AverageNs"])
+            out["trace_calls"] = int(r["Calls"])
+(dst / f"{rnd}_{wl}_pmc.json").write_text(json.dumps(out, indent=1))
+print(json.dumps(out, indent=1))
