@@ -13,7 +13,7 @@ import os
 from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
-LIB_PATH = PKG / "libmsa.so"
+LIB_PATH = Path(os.environ.get("MSA_LIB_PATH", PKG / "libmsa.so"))  # override: diagnostic builds only
 
 MSA_OK = 0
 STATUS = {
@@ -89,6 +89,7 @@ def lib() -> C.CDLL:
     L.msa_plan_stripe_meta.argtypes = [P, P, i64, P]
     L.msa_plan_stripes.argtypes = [P]
     L.msa_plan_stripes.restype = i64
+    L.msa_plan_pair_layout.argtypes = [P, i64, C.POINTER(i64)]
     L.msa_plan_checksum.argtypes = [P, P, i64, C.POINTER(u64), P]
     L.msa_plan_last_kernel_ms.argtypes = [P, C.POINTER(C.c_float)]
     L.msa_encode_pair.argtypes = [P, sz, P, sz, P, P]
@@ -112,6 +113,7 @@ class _Bind:
 EXPORTED = [
     "msa_status_string", "msa_version", "msa_device_count", "msa_main_alignment", "msa_subproblem",
     "msa_partial_partition", "msa_partial_tables", "msa_plan_create", "msa_plan_destroy", "msa_plan_cells_size",
-    "msa_plan_run", "msa_plan_results", "msa_plan_stripe_meta", "msa_plan_stripes", "msa_plan_checksum",
+    "msa_plan_run", "msa_plan_results", "msa_plan_stripe_meta", "msa_plan_stripes", "msa_plan_pair_layout",
+    "msa_plan_checksum",
     "msa_plan_last_kernel_ms", "msa_encode_pair", "msa_sw_align",
 ]

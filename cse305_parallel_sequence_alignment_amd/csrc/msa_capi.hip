@@ -64,7 +64,11 @@ int nc_of(int alg) {
 typedef void (*kfn_t)(KArgs);
 
 template <int ALG, int OUT, bool TP>
-kfn_t kf(int W) { return W == MSA_WAVES_SINGLE ? stripe_kernel<ALG, OUT, TP, MSA_WAVES_SINGLE> : stripe_kernel<ALG, OUT, TP, MSA_WAVES_BATCH>; }
+kfn_t kf(int W) {
+  // single pair: (MSA_WAVES_SINGLE waves, MSA_KS_SINGLE steps/phase); batch: (MSA_WAVES_BATCH, MSA_KS_BATCH)
+  return W == MSA_WAVES_SINGLE ? stripe_kernel<ALG, OUT, TP, MSA_WAVES_SINGLE, MSA_KS_SINGLE>
+                               : stripe_kernel<ALG, OUT, TP, MSA_WAVES_BATCH, MSA_KS_BATCH>;
+}
 
 kfn_t pick_kernel(int alg, int out, int tp, int W) {
 #define K3(A, O) return tp ? kf<A, O, true>(W) : kf<A, O, false>(W)
@@ -103,6 +107,7 @@ struct msa_plan {
   msa_kparams kp;
   int nc = 1;
   int W = MSA_WAVES_BATCH;  // compute waves per workgroup
+  int KS = MSA_KS_BATCH;    // DP steps per phase
   std::vector<msa_pair_desc> pairs;
   int64_t total_stripes = 0;
   int64_t cells_elems = 0;
@@ -195,6 +200,8 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   const int tp = (kalg == MSA_ALG_SWL || kalg == MSA_ALG_SWA) ? (desc->track_end ? 1 : 0) : 0;
   const int W = desc->single ? MSA_WAVES_SINGLE : MSA_WAVES_BATCH;
   P->W = W;
+  const int KS = desc->single ? MSA_KS_SINGLE : MSA_KS_BATCH;
+  P->KS = KS;
   P->fn = pick_kernel(kalg, out_mode, tp, W);
   if (!P->fn) { delete P; return MSA_ERR_UNSUPPORTED; }
   if (desc->single && desc->n_pairs != 1) { delete P; return MSA_ERR_ARG; }
@@ -241,10 +248,10 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
       int cmin = 1 << 30, cmax = -(1 << 30);
       for (int k = k0; k < std::min(S, k0 + per_item); ++k) {
         StripeGeom g;
-        stripe_geom(k, (int)m, (int)n, band, g);
-        pmax = std::max(pmax, g.P);
+        stripe_geom(k, (int)m, (int)n, band, g, KS);
+        pmax = std::max(pmax, g.P * (KS / MSA_K));  // in 16-step layout blocks
         cmin = std::min(cmin, g.cs - 64);
-        cmax = std::max(cmax, g.cs + g.P * MSA_K);
+        cmax = std::max(cmax, g.cs + g.P * KS);
       }
       cmin &= ~3;
       max_code = std::max(max_code, cmax - cmin + 8);
@@ -266,7 +273,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   P->total_stripes = stripe0;
   P->cells_elems = off;
   kp.sched_cap = desc->single ? W : max_S;
-  kp.lds_code_bytes = ((max_code + 16) + 15) & ~15;
+  kp.lds_code_bytes = ((max_code + 48) + 15) & ~15;  // + slack: the prefetch of phase P reads past the window
   kp.lds_row_words = desc->single ? 0 : (((max_P * MSA_K + MSA_ROWOFF + 32) + 15) & ~15);
   if (desc->single) {
     const int S = (int)((desc->m[0] + 63) / 64);
@@ -340,6 +347,16 @@ int msa_plan_cells_size(const msa_plan* P, int64_t* elems) {
 }
 
 int64_t msa_plan_stripes(const msa_plan* P) { return P ? P->total_stripes : 0; }
+
+int msa_plan_pair_layout(const msa_plan* P, int64_t pair, int64_t* out4) {
+  if (!P || !out4 || pair < 0 || pair >= (int64_t)P->pairs.size()) return MSA_ERR_ARG;
+  const msa_pair_desc& pd = P->pairs[(size_t)pair];
+  out4[0] = pd.stripe0;
+  out4[1] = pd.pmax;
+  out4[2] = pd.out_off;
+  out4[3] = P->KS;
+  return MSA_OK;
+}
 
 int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, void* c1, void* c2, void* stream) {
   if (!P || !dA || !dB) return MSA_ERR_ARG;

@@ -41,9 +41,13 @@
 
 #include "msa_types.h"
 
+#ifndef MSA_WAVES_SINGLE
 #define MSA_WAVES_SINGLE 4  // single pair: one compute wave per SIMD (latency-bound wavefront)
+#endif
+#define MSA_KS_SINGLE 32  // steps per phase, single pair: fewer phases amortise the per-phase sync
+#define MSA_KS_BATCH 16   // steps per phase, batch: fewer registers, two workgroups per CU
 #define MSA_WAVES_BATCH 8   // batch: two per SIMD (throughput-bound, hides the step chain)
-#define MSA_K 16
+#define MSA_K 16  // output layout block: cells are stored in blocks of 16 steps (any KS is a multiple)
 #define MSA_RING 256
 #define MSA_ROWOFF 128
 #define MSA_GOFF 128
@@ -62,6 +66,10 @@ template <> struct Tr<MSA_ALG_PART> { static constexpr int NC = 3; };
 
 __device__ __forceinline__ int dpp_shr1(int old, int src) {
   return __builtin_amdgcn_update_dpp(old, src, 0x138, 0xf, 0xf, false);
+}
+// wave_shl:1 -- lane l takes lane l+1, lane 63 keeps `old`
+__device__ __forceinline__ int dpp_shl1(int old, int src) {
+  return __builtin_amdgcn_update_dpp(old, src, 0x130, 0xf, 0xf, false);
 }
 __host__ __device__ __forceinline__ int imax(int a, int b) { return a > b ? a : b; }
 __device__ __forceinline__ int imax3(int a, int b, int c) { return imax(imax(a, b), c); }
@@ -85,7 +93,7 @@ __host__ __device__ __forceinline__ int jlo_of(int i, int band) { return band < 
 __host__ __device__ __forceinline__ int jhi_of(int i, int n, int band) { return band < 0 ? n : (i + band < n ? i + band : n); }
 
 // Geometry of pair-local stripe k (rows 64k+1 .. 64k+64).
-__host__ __device__ inline void stripe_geom(int k, int m, int n, int band, StripeGeom& g) {
+__host__ __device__ inline void stripe_geom(int k, int m, int n, int band, StripeGeom& g, int KS) {
   const int i0 = 64 * k + 1;
   const int rlast = (m - 64 * k - 1 < 63) ? (m - 64 * k - 1) : 63;
   const int ilast = i0 + rlast;
@@ -96,7 +104,7 @@ __host__ __device__ inline void stripe_geom(int k, int m, int n, int band, Strip
   g.lead = lead;
   g.cs = clo - lead;
   const int tmax_max = jhi_of(ilast, n, band) - g.cs + rlast;
-  g.P = tmax_max / MSA_K + 1;
+  g.P = tmax_max / KS + 1;  // phases of KS steps
   g.mask_lo = jlo_of(ilast, band) - g.cs + rlast;  // max over rows of tmin
   g.mask_hi = jhi_of(i0, n, band) - g.cs;          // min over rows of tmax
   g.c_hi = jhi_of(ilast, n, band);
@@ -356,13 +364,38 @@ enum Snk { SNK_NONE = 0, SNK_RING = 1, SNK_ROW = 2, SNK_GLOBAL = 3 };
 // vmcnt(0) right after a load.
 #define MSA_LOAD_AHEAD 4
 
+// Phase barrier.  The diagnostic build (-DMSA_STAMPS) records s_memtime just
+// before and after every barrier of every wave: stamps[((item*16 + wave)*4096
+// + phase)*2 + {0,1}] (phases >= 4096 and items >= 64 are not recorded).
+#ifdef MSA_STAMPS
+#define MSA_SYNC(ph_)                                                                       \
+  do {                                                                                      \
+    const int ph__ = (ph_);                                                                 \
+    const bool rec__ = a.stamps && lane == 0 && ph__ < 4096 && item < 64;                   \
+    const size_t o__ = (((size_t)item * 16 + w) * 4096 + ph__) * 4;                          \
+    if (rec__) a.stamps[o__] = __builtin_amdgcn_s_memtime();                                \
+    __syncthreads();                                                                        \
+    if (rec__) a.stamps[o__ + 1] = __builtin_amdgcn_s_memtime();                            \
+  } while (0)
+#define MSA_MARK(ph_, slot_)                                                                \
+  do {                                                                                      \
+    const int ph__ = (ph_);                                                                 \
+    if (a.stamps && lane == 0 && ph__ < 4096 && item < 64)                                  \
+      a.stamps[(((size_t)item * 16 + w) * 4096 + ph__) * 4 + (slot_)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define MSA_SYNC(ph_) __syncthreads()
+#define MSA_MARK(ph_, slot_) do {} while (0)
+#endif
+
+// c = 16-column chunk index of the item's first stripe (nch chunks in all).
 template <int NC>
-__device__ __forceinline__ void loader_commit(const KArgs& a, const StripeGeom& s0, int q, unsigned long long gv,
+__device__ __forceinline__ void loader_commit(const KArgs& a, int cs0, int nch, int q, unsigned long long gv,
                                               const unsigned long long* g_in, int* stage, int chi, int n,
                                               unsigned ep, int lane) {
   const int v = lane >> 4, l = lane & 15;
-  const int col = s0.cs + 16 * q + l;
-  const bool need = (v < NC) && (col <= chi) && (col <= n) && (q < s0.P);
+  const int col = cs0 + 16 * q + l;
+  const bool need = (v < NC) && (col <= chi) && (col <= n) && (q < nch);
   bool ok = !need || ((unsigned)(gv >> 32) == ep);
   unsigned spins = 0;
   while (!__all(ok)) {
@@ -380,21 +413,23 @@ __device__ __forceinline__ void loader_commit(const KArgs& a, const StripeGeom& 
 }
 
 template <int NC>
-__device__ __forceinline__ unsigned long long loader_issue(const KArgs& a, const StripeGeom& s0, int q,
+__device__ __forceinline__ unsigned long long loader_issue(const KArgs& a, int cs0, int q,
                                                            const unsigned long long* g_in, int lane) {
   const int v = min(lane >> 4, NC - 1), l = lane & 15;
-  const int col = min(s0.cs + 16 * q + l, a.gbuf_stride - 1 - MSA_GOFF);
+  const int col = min(cs0 + 16 * q + l, a.gbuf_stride - 1 - MSA_GOFF);
   return gload(g_in + (size_t)v * a.gbuf_stride + col + MSA_GOFF);
 }
 
-template <int ALG, int OUT, bool TRACKPOS, int W>
+template <int ALG, int OUT, bool TRACKPOS, int W, int KS>
 __global__ __launch_bounds__((W + 1) * 64) void stripe_kernel(KArgs a) {
+  static_assert(KS % 16 == 0 && KS <= 64, "phases are whole 16-step layout blocks");
+  constexpr int CPP = KS / 16;  // 16-column chunks per phase
   constexpr int NC = Tr<ALG>::NC;
   // Smith-Waterman kernels never mask: columns outside [1, n] carry the
   // virtual code whose score (MSA_VIRT_SCORE) keeps every out-of-matrix cell
   // strictly below a real cell, so the plain recurrence runs over them.
   constexpr bool SWK = (ALG == MSA_ALG_SWL || ALG == MSA_ALG_SWA);
-  constexpr int LA = MSA_LOAD_AHEAD;
+  constexpr int LA = (MSA_LOAD_AHEAD * 16 + KS - 1) / KS;  // loader prefetch depth in phases
   extern __shared__ __attribute__((aligned(16))) int smem[];
   const msa_kparams& kp = a.kp;
   const int lane = threadIdx.x & 63;
@@ -444,10 +479,13 @@ __global__ __launch_bounds__((W + 1) * 64) void stripe_kernel(KArgs a) {
       StripeGeom prev;
       for (int k = 0; k < ns; ++k) {
         StripeGeom g;
-        stripe_geom(k0 + k, m, n, kp.band, g);
+        stripe_geom(k0 + k, m, n, kp.band, g, KS);
         int T = 0;
         if (k > 0) {
-          const int D = (g.cs - prev.cs + 78) / MSA_K + 1;  // cs diff >= -15 -> numerator > 0
+          // the consumer's phase q reads producer columns up to cs+KS*q+KS-1,
+          // computed at producer step (cs - prev.cs + 63) + KS*q + KS-1; that
+          // phase must be complete (one barrier) first.  cs diff >= -15.
+          const int D = (g.cs - prev.cs + 62 + KS) / KS + 1;
           T = prev.T + D;
           if (k >= W) {
             const StripeGeom& o = sched[k - W];
@@ -459,7 +497,7 @@ __global__ __launch_bounds__((W + 1) * 64) void stripe_kernel(KArgs a) {
         prev = g;
         total = max(total, T + g.P);
         cmin = min(cmin, g.cs - 64);
-        cmax = max(cmax, g.cs + g.P * MSA_K);
+        cmax = max(cmax, g.cs + g.P * KS);
       }
       misc[1] = total;
       misc[2] = cmin & ~3;  // code window base column (multiple of 4)
@@ -498,26 +536,67 @@ __global__ __launch_bounds__((W + 1) * 64) void stripe_kernel(KArgs a) {
       int chi = n;
       if (k0 > 0) {
         StripeGeom gp;
-        stripe_geom(k0 - 1, m, n, kp.band, gp);
+        stripe_geom(k0 - 1, m, n, kp.band, gp, KS);
         chi = gp.c_hi;
       }
       const unsigned long long* g_in = act ? a.gbuf + (size_t)(group - 1) * NC * a.gbuf_stride : a.gbuf;
       const bool border = (k0 == 0);  // the item holds the pair's first stripe: stage the DP's row 0
-      auto commit_border = [&](int q) {
+      // all staging / sinking works in 16-column chunks; phase p = chunks [CPP*p, CPP*p + CPP)
+      const int nch0 = s0.P * CPP;
+      auto commit_border = [&](int c) {
         const int v = lane >> 4, l = lane & 15;
         int bv[3];
-        border_top<ALG>(kp, s0.cs + 16 * q + l, bv);
+        border_top<ALG>(kp, s0.cs + 16 * c + l, bv);
         const int val = (v == 0) ? bv[0] : (v == 1 ? bv[1] : bv[2]);
-        if (v < NC) stage[v * MSA_RING + ((16 * q + l) & (MSA_RING - 1))] = val;
+        if (v < NC) stage[v * MSA_RING + ((16 * c + l) & (MSA_RING - 1))] = val;
       };
-      if (border) commit_border(0);
-      unsigned long long G[LA];
+      // Sink: the item's last stripe hands its bottom row to the next
+      // workgroup.  Its compute wave only writes its LDS ring; this wave
+      // publishes the KS columns of each phase as {epoch, value} granules
+      // one phase later (after the barrier that completes them).
+      const int sl_idx = ns - 1;
+      // (with the DPP shift register the compute wave publishes itself)
+      const bool sink = kp.single && (k0 + sl_idx) < S_pair - 1 && !(NC == 1 && KS > 16);
+      StripeGeom sl = sched[sl_idx];
+      sl.T = uni(sl.T); sl.P = uni(sl.P); sl.cs = uni(sl.cs);
+      int sl_out_cs = 0;
+      if (sink) {
+        StripeGeom gn;
+        stripe_geom(k0 + sl_idx + 1, m, n, kp.band, gn, KS);
+        sl_out_cs = uni(gn.cs);
+      }
+      const int* ring_last = rings + ((((sl_idx / W) & 1) * W + sl_idx % W) * NC) * MSA_RING;
+      unsigned long long* g_out = a.gbuf + (size_t)group * NC * a.gbuf_stride;
+      auto sink_phase = [&](int q) {
+        if (!sink || q < 0 || q >= sl.P) return;
+        const int v = lane >> 4, l = lane & 15;
+        if (v < NC) {
+#pragma unroll
+          for (int h = 0; h < CPP; ++h) {
+            const int x = sl.cs + KS * q + 16 * h - 63 - sl_out_cs + l;
+            const int col = sl.cs + KS * q + 16 * h - 63 + l;
+            if (col + MSA_GOFF >= 0 && col + MSA_GOFF < a.gbuf_stride) {
+              const int val = ring_last[v * MSA_RING + (x & (MSA_RING - 1))];
+              gstore(g_out + (size_t)v * a.gbuf_stride + col + MSA_GOFF,
+                     ((unsigned long long)ep << 32) | (unsigned)val);
+            }
+          }
+        }
+      };
+      // Staging runs one phase ahead of the compute waves: phase 0 before
+      // the first barrier, phase p+1 during phase p.
+      if (border) {
+#pragma unroll
+        for (int h = 0; h < CPP; ++h) commit_border(h);
+      }
+      constexpr int NS = LA * CPP;  // prefetch slots; slot c % NS holds the load of chunk c
+      unsigned long long G[NS];
       if (act) {
-        // start only once the producer is LA+2 phases ahead, so that every
+        // start only once the producer is LA+1 phases ahead, so that every
         // prefetch below reads an already-published granule (no re-poll stalls)
         {
-          const int qw = min(s0.P - 1, LA + 1);
-          const int colw = min(min(s0.cs + 16 * qw + 15, chi), n);
+          const int cw_ = min(nch0 - 1, (LA + 2) * CPP - 1);
+          const int colw = min(min(s0.cs + 16 * cw_ + 15, chi), n);
           unsigned spins = 0;
           while ((unsigned)(gload(g_in + colw + MSA_GOFF) >> 32) != ep) {
             __builtin_amdgcn_s_sleep(2);
@@ -528,8 +607,12 @@ __global__ __launch_bounds__((W + 1) * 64) void stripe_kernel(KArgs a) {
           }
         }
 #pragma unroll
-        for (int s = 0; s < LA; ++s) G[s] = loader_issue<NC>(a, s0, s, g_in, lane);
-        loader_commit<NC>(a, s0, 0, G[0], g_in, stage, chi, n, ep, lane);
+        for (int c = 0; c < NS; ++c) G[c] = loader_issue<NC>(a, s0.cs, c, g_in, lane);
+#pragma unroll
+        for (int h = 0; h < CPP; ++h) {
+          loader_commit<NC>(a, s0.cs, nch0, h, G[h], g_in, stage, chi, n, ep, lane);
+          G[h] = loader_issue<NC>(a, s0.cs, NS + h, g_in, lane);
+        }
       }
       __syncthreads();  // phase 0 staged before any compute wave reads it
       for (int ph = 0; ph < total; ph += LA) {
@@ -538,15 +621,27 @@ __global__ __launch_bounds__((W + 1) * 64) void stripe_kernel(KArgs a) {
           const int p = ph + s;
           if (p < total) {
             if (act) {
-              if (p + 1 < s0.P) loader_commit<NC>(a, s0, p + 1, G[(s + 1) % LA], g_in, stage, chi, n, ep, lane);
-              if (p + LA < s0.P) G[s] = loader_issue<NC>(a, s0, p + LA, g_in, lane);
+              if (p + 1 < s0.P) {
+#pragma unroll
+                for (int h = 0; h < CPP; ++h) {
+                  const int c = (p + 1) * CPP + h;
+                  const int slot = ((s + 1) % LA) * CPP + h;
+                  loader_commit<NC>(a, s0.cs, nch0, c, G[slot], g_in, stage, chi, n, ep, lane);
+                  if (c + NS < nch0) G[slot] = loader_issue<NC>(a, s0.cs, c + NS, g_in, lane);
+                }
+              }
             } else if (border) {
-              if (p + 1 < s0.P) commit_border(p + 1);
+              if (p + 1 < s0.P) {
+#pragma unroll
+                for (int h = 0; h < CPP; ++h) commit_border((p + 1) * CPP + h);
+              }
             }
-            __syncthreads();
+            sink_phase(p - 1 - sl.T);  // the last stripe's phase completed by the previous barrier
+            MSA_SYNC(p);
           }
         }
       }
+      sink_phase(total - 1 - sl.T);
       continue;
     }
 
@@ -561,7 +656,7 @@ __global__ __launch_bounds__((W + 1) * 64) void stripe_kernel(KArgs a) {
       StripeGeom sg = sched[cur];
       sg.T = uni(sg.T); sg.P = uni(sg.P); sg.cs = uni(sg.cs); sg.lead = uni(sg.lead);
       sg.mask_lo = uni(sg.mask_lo); sg.mask_hi = uni(sg.mask_hi); sg.c_hi = uni(sg.c_hi);
-      for (; ph < sg.T; ++ph) __syncthreads();
+      for (; ph < sg.T; ++ph) MSA_SYNC(ph);
       // ---- stripe init ----
       const int ks = k0 + cur;  // pair-local stripe index
       LaneState<ALG> L;
@@ -632,63 +727,81 @@ __global__ __launch_bounds__((W + 1) * 64) void stripe_kernel(KArgs a) {
       int out_cs = 0;
       if (snk != SNK_NONE) {
         StripeGeom gn;
-        stripe_geom(ks + 1, m, n, kp.band, gn);
+        stripe_geom(ks + 1, m, n, kp.band, gn, KS);
         out_cs = gn.cs;
       }
       int out_chi = n;  // c_hi of the producer row above (input masking, banded)
       if (ks > 0) {
         StripeGeom gp;
-        stripe_geom(ks - 1, m, n, kp.band, gp);
+        stripe_geom(ks - 1, m, n, kp.band, gp, KS);
         out_chi = gp.c_hi;
       }
       snk = uni(snk); out_cs = uni(out_cs); out_chi = uni(out_chi);
-      unsigned long long* const g_out = (snk == SNK_GLOBAL) ? a.gbuf + (size_t)group * NC * a.gbuf_stride : nullptr;
-      const size_t obase = (size_t)pd.out_off + (size_t)ks * pd.pmax * MSA_K * 64;
+      unsigned long long* const g_out = a.gbuf + (size_t)group * NC * a.gbuf_stride;
+      const size_t obase = (size_t)pd.out_off + (size_t)ks * pd.pmax * MSA_K * 64;  // pmax: 16-step blocks
 
       auto run_phase = [&](const int q, auto MASKED_, auto INMASK_) {
         constexpr bool MASKED = decltype(MASKED_)::value;  // per-lane start/end checks
         constexpr bool INMASK = decltype(INMASK_)::value;  // input columns beyond the producer's last
-
         // ---- all LDS reads of the phase up front (one exposed latency per phase) ----
-        int IN[NC][16];
+        int IN[NC][KS];
         {
-          const int* base = in_ptr + ((16 * q) & in_mask);
+          const int* base = in_ptr + ((KS * q) & in_mask);
 #pragma unroll
           for (int v = 0; v < NC; ++v) {
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < KS / 4; ++u) {
+#ifdef MSA_DBG_NO_IN
+              const int4 x = make_int4(q, q + 1, q + 2, u);
+#else
               const int4 x = *reinterpret_cast<const int4*>(base + v * in_vs + 4 * u);
+#endif
               IN[v][4 * u + 0] = x.x; IN[v][4 * u + 1] = x.y; IN[v][4 * u + 2] = x.z; IN[v][4 * u + 3] = x.w;
             }
           }
           if constexpr (INMASK) {
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {
-              const bool o = sg.cs + 16 * q + k > out_chi;
+            for (int k = 0; k < KS; ++k) {
+              const bool o = sg.cs + KS * q + k > out_chi;
 #pragma unroll
               for (int v = 0; v < NC; ++v) IN[v][k] = o ? MSA_NEG : IN[v][k];
             }
           }
         }
-        unsigned cw[4];
+        unsigned cw[KS / 4];
         {
-          const unsigned* cp = codes + L.cw_base + 4 * q;  // per-lane, dword aligned only
-          cw[0] = cp[0]; cw[1] = cp[1]; cw[2] = cp[2]; cw[3] = cp[3];
-        }
-        int hist[NC][16];
-        int hv[16];
-        unsigned dirw[4] = {0u, 0u, 0u, 0u};
-        int4* hrow = reinterpret_cast<int4*>(a.outH + obase) + (size_t)(4 * q) * 64 + lane;
-        int4* t2row = reinterpret_cast<int4*>(a.outT2 + obase) + (size_t)(4 * q) * 64 + lane;
-        int4* t3row = reinterpret_cast<int4*>(a.outT3 + obase) + (size_t)(4 * q) * 64 + lane;
+          const unsigned* cp = codes + L.cw_base + (KS / 4) * q;  // per-lane, dword aligned only
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+          for (int u = 0; u < KS / 4; ++u) {
+#ifdef MSA_DBG_NO_CW
+            cw[u] = (unsigned)(L.cw_base + q * 0x01010101 + u);
+#else
+            cw[u] = cp[u];
+#endif
+          }
+        }
+        int hist[NC][KS];
+        int hv[KS];
+        unsigned dirw[KS / 4];
+        // NC == 1: lane 63's carried value is collected by a DPP shift register
+        // (one wave_shl per step: after KS steps lane 64-KS+k holds step k),
+        // so the hand-off is ONE ds_write_b32 of KS lanes per phase instead of
+        // KS/4 single-lane b128 writes that all waves issue at once.
+        // (single-pair kernels only: in batch the SIMDs are saturated and the
+        // extra DPP per step costs more than the lockstep writes)
+        constexpr bool SHREG = (NC == 1) && (KS > 16);
+        int shreg = 0;
+        int4* hrow = reinterpret_cast<int4*>(a.outH + obase) + (size_t)((KS / 4) * q) * 64 + lane;
+        int4* t2row = reinterpret_cast<int4*>(a.outT2 + obase) + (size_t)((KS / 4) * q) * 64 + lane;
+        int4* t3row = reinterpret_cast<int4*>(a.outT3 + obase) + (size_t)((KS / 4) * q) * 64 + lane;
+#pragma unroll
+        for (int u = 0; u < KS / 4; ++u) {
           const unsigned s4 = __builtin_amdgcn_perm(L.phi, L.plo, cw[u]);
           unsigned dq = 0;
 #pragma unroll
           for (int kk = 0; kk < 4; ++kk) {
             const int k = 4 * u + kk;
-            const int t = 16 * q + k;
+            const int t = KS * q + k;
             const int s = ((int)(s4 << (24 - 8 * kk))) >> 24;
             int inv[3];
 #pragma unroll
@@ -699,6 +812,7 @@ __global__ __launch_bounds__((W + 1) * 64) void stripe_kernel(KArgs a) {
             const unsigned d = step<ALG, OUT, MASKED, TRACKPOS>(kp, L, inv, s, t, ct, cr, hv[k]);
 #pragma unroll
             for (int v = 0; v < NC; ++v) hist[v][k] = cr[v];
+            if constexpr (SHREG) shreg = dpp_shl1(cr[0], shreg);
             dq |= d << (8 * kk);
           }
           dirw[u] = dq;
@@ -723,72 +837,70 @@ __global__ __launch_bounds__((W + 1) * 64) void stripe_kernel(KArgs a) {
           }
         }
         if constexpr (OUT == MSA_OUT_DIR) {
-          reinterpret_cast<uint4*>(a.outDir + obase)[(size_t)q * 64 + lane] =
-              make_uint4(dirw[0], dirw[1], dirw[2], dirw[3]);
+#pragma unroll
+          for (int h = 0; h < CPP; ++h)
+            reinterpret_cast<uint4*>(a.outDir + obase)[(size_t)(CPP * q + h) * 64 + lane] =
+                make_uint4(dirw[4 * h], dirw[4 * h + 1], dirw[4 * h + 2], dirw[4 * h + 3]);
         }
+        MSA_MARK(ph + q, 2);
         // hand the bottom row to the next stripe: lane 63, once per phase
-        if (snk != SNK_NONE && lane == 63) {
-          const int x = (sg.cs + 16 * q - 63 - out_cs + out_add) & out_mask;  // multiple of 16
-          if (x >= 0 && x + 12 <= out_lim) {
-            int* dst = out_ptr + x;
-#pragma unroll
-            for (int v = 0; v < NC; ++v)
-#pragma unroll
-              for (int u = 0; u < 4; ++u)
-                *reinterpret_cast<int4*>(dst + v * out_vs + 4 * u) =
-                    make_int4(hist[v][4 * u], hist[v][4 * u + 1], hist[v][4 * u + 2], hist[v][4 * u + 3]);
+        if constexpr (SHREG) {
+          if (snk != SNK_NONE && lane >= 64 - KS) {
+            const int kk_ = lane - (64 - KS);
+            if (snk == SNK_GLOBAL) {
+              // last stripe of the item: publish straight to the next workgroup
+              const int col = sg.cs + KS * q - 63 + kk_;
+              if (col + MSA_GOFF >= 0 && col + MSA_GOFF < a.gbuf_stride)
+                gstore(g_out + col + MSA_GOFF, ((unsigned long long)ep << 32) | (unsigned)shreg);
+            } else {
+              const int x = sg.cs + KS * q - 63 - out_cs + out_add + kk_;
+              const int xm = x & out_mask;
+              if (x >= 0 && xm < out_lim + 4) out_ptr[xm] = shreg;
+            }
           }
-        }
-        // global sink: 8-byte {epoch, value} granules for the 16 columns of this phase
-        if (snk == SNK_GLOBAL) {
-          asm volatile("" ::: "memory");  // lane 63's ring writes stay ahead of these reads
-          const int v = lane >> 4, l = lane & 15;
-          if (v < NC) {
-            const int x = sg.cs + 16 * q - 63 - out_cs + l;
-            const int col = sg.cs + 16 * q - 63 + l;
-            if (col + MSA_GOFF >= 0 && col + MSA_GOFF < a.gbuf_stride) {
-              const int val = ring_out[v * MSA_RING + (x & (MSA_RING - 1))];
-              gstore(g_out + (size_t)v * a.gbuf_stride + col + MSA_GOFF, ((unsigned long long)ep << 32) | (unsigned)val);
+        } else if (snk != SNK_NONE && lane == 63) {
+          // (in 16-column chunks: the ring offset is only 16-aligned, each chunk wraps on its own)
+#pragma unroll
+          for (int h = 0; h < CPP; ++h) {
+            const int x = (sg.cs + KS * q + 16 * h - 63 - out_cs + out_add) & out_mask;  // multiple of 16
+            if (x >= 0 && x + 12 <= out_lim) {
+              int* dst = out_ptr + x;
+#pragma unroll
+              for (int v = 0; v < NC; ++v)
+#pragma unroll
+                for (int u = 4 * h; u < 4 * h + 4; ++u)
+                  *reinterpret_cast<int4*>(dst + v * out_vs + 4 * (u - 4 * h)) =
+                      make_int4(hist[v][4 * u], hist[v][4 * u + 1], hist[v][4 * u + 2], hist[v][4 * u + 3]);
             }
           }
         }
       };
       using T_ = std::true_type;
       using F_ = std::false_type;
-      // phase q needs no range checks iff 16q >= mask_lo (every lane has
-      // started), 16q+15 <= mask_hi (none has finished) and every input column
-      // cs+16q+15 <= out_chi
+      // phase q needs no range checks iff KS*q >= mask_lo (every lane has
+      // started), KS*q+KS-1 <= mask_hi (none has finished) and every input
+      // column cs+KS*q+KS-1 <= out_chi
       const int P = sg.P;
-      const int lim = min(sg.mask_hi, out_chi - sg.cs) - 15;
-      const int qa = uni(min(P, sg.mask_lo <= 0 ? 0 : (sg.mask_lo + 15) / 16));
-      const int qb = uni(max(qa, min(P, lim >= 0 ? lim / 16 + 1 : 0)));
-      int q = 0;
+      const int lim = min(sg.mask_hi, out_chi - sg.cs) - (KS - 1);
+      const int qa = uni(min(P, sg.mask_lo <= 0 ? 0 : (sg.mask_lo + KS - 1) / KS));
+      const int qb = uni(max(qa, min(P, lim >= 0 ? lim / KS + 1 : 0)));
+      auto run_range = [&](const int qb_, const int qe_, auto MASKED_, auto INMASK_) {
+        for (int q = qb_; q < qe_; ++q) {
+          run_phase(q, MASKED_, INMASK_);
+          MSA_SYNC(ph + q);
+        }
+      };
       if constexpr (SWK) {
         // no state masking; only the inputs past the producer's last column
         // (never written into the ring / granules) are replaced by -inf
-        const int li = out_chi - sg.cs - 15;
-        const int qi = uni(min(P, li >= 0 ? li / 16 + 1 : 0));
-        for (; q < qi; ++q) {
-          run_phase(q, F_{}, F_{});
-          __syncthreads();
-        }
-        for (; q < P; ++q) {
-          run_phase(q, F_{}, T_{});
-          __syncthreads();
-        }
+        const int li = out_chi - sg.cs - (KS - 1);
+        const int qi = uni(min(P, li >= 0 ? li / KS + 1 : 0));
+        run_range(0, qi, F_{}, F_{});
+        run_range(qi, P, F_{}, T_{});
       } else {
-        for (; q < qa; ++q) {
-          run_phase(q, T_{}, T_{});
-          __syncthreads();
-        }
-        for (; q < qb; ++q) {
-          run_phase(q, F_{}, F_{});
-          __syncthreads();
-        }
-        for (; q < P; ++q) {
-          run_phase(q, T_{}, T_{});
-          __syncthreads();
-        }
+        run_range(0, qa, T_{}, T_{});
+        run_range(qa, qb, F_{}, F_{});
+        run_range(qb, P, T_{}, T_{});
       }
       ph += P;
       // ---- stripe finalize ----
@@ -820,10 +932,10 @@ __global__ __launch_bounds__((W + 1) * 64) void stripe_kernel(KArgs a) {
       }
       if (lane == 0) {
         md->cs = sg.cs;
-        md->phases = sg.P;
+        md->phases = sg.P * CPP;  // in 16-step layout blocks
       }
     }
-    for (; ph < total; ++ph) __syncthreads();
+    for (; ph < total; ++ph) MSA_SYNC(ph);
   }
 }
 

@@ -69,16 +69,13 @@ class Plan:
         LB.check(L.msa_plan_cells_size(self._h, C.byref(e)), "msa_plan_cells_size")
         self.cells_elems = e.value
         self.n_stripes = int(L.msa_plan_stripes(self._h))
-        # host copy of the geometry (same formulas as the C side)
+        # per-pair layout as the C side laid it out
         self.geom = []
-        s0, off = 0, 0
-        for m, n in zip(self.ms, self.ns):
-            S = (m + 63) // 64
-            pmax = max(stripe_phases(k, m, n, band if alg == LB.NW_BANDED else -1) for k in range(S))
-            self.geom.append(PairGeom(m, n, s0, pmax, off))
-            cells_ = S * pmax * 16 * 64
-            off += (cells_ + 63) & ~63
-            s0 += S
+        lay = (C.c_int64 * 4)()
+        for k, (m, n) in enumerate(zip(self.ms, self.ns)):
+            LB.check(L.msa_plan_pair_layout(self._h, k, lay), "msa_plan_pair_layout")
+            self.geom.append(PairGeom(m, n, int(lay[0]), int(lay[1]), int(lay[2])))
+        self.phase_steps = int(lay[3])
 
     def __del__(self):
         try:
@@ -162,8 +159,8 @@ def jhi_of(i: int, n: int, band: int) -> int:
     return n if band < 0 else min(n, i + band)
 
 
-def stripe_geom(k: int, m: int, n: int, band: int):
-    """Python restatement of stripe_geom() (msa_kernels.hip): (cs, P) of pair-local stripe k.
+def stripe_geom(k: int, m: int, n: int, band: int, ks: int = 16):
+    """Python restatement of stripe_geom() (msa_kernels.hip): (cs, P) of pair-local stripe k, P in phases of ks steps.
 
     Lane r of stripe k (row 64k+r+1) processes column cs + t - r at step t,
     t in [0, 16P); cs is chosen so that cs = c_lo - lead with
@@ -174,8 +171,8 @@ def stripe_geom(k: int, m: int, n: int, band: int):
     clo = jlo_of(i0, band)
     lead = (clo - 1 - k) % 16 + 1
     cs = clo - lead
-    return cs, (jhi_of(ilast, n, band) - cs + rlast) // 16 + 1
+    return cs, (jhi_of(ilast, n, band) - cs + rlast) // ks + 1
 
 
-def stripe_phases(k: int, m: int, n: int, band: int) -> int:
-    return stripe_geom(k, m, n, band)[1]
+def stripe_phases(k: int, m: int, n: int, band: int, ks: int = 16) -> int:
+    return stripe_geom(k, m, n, band, ks)[1]

@@ -58,17 +58,18 @@ def test_stripe_phases_cover_every_cell():
     """Stripe s (rows 64s+1..64s+64) runs 16*phases anti-diagonal steps covering columns jlo..jhi of each row."""
     from cse305_parallel_sequence_alignment_amd.plan import jhi_of, jlo_of, stripe_geom
 
-    for (m, n, band) in [(1, 1, -1), (64, 64, -1), (65, 100, -1), (700, 650, -1), (1000, 1000, 32), (500, 900, 512)]:
+    for (m, n, band, ks) in [(1, 1, -1, 16), (64, 64, -1, 16), (65, 100, -1, 32), (700, 650, -1, 16), (700, 650, -1, 32),
+                             (1000, 1000, 32, 16), (500, 900, 512, 32)]:
         S = (m + 63) // 64
         for s in range(S):
-            cs, P = stripe_geom(s, m, n, band)
+            cs, P = stripe_geom(s, m, n, band, ks)
             for r in range(min(64, m - 64 * s)):
                 i = 64 * s + r + 1
                 jl, jh = jlo_of(i, band), jhi_of(i, n, band)
                 if jl > jh:
                     continue
                 # lane r processes column cs + t - r at step t
-                assert cs + 0 - r <= jl and cs + 16 * P - 1 - r >= jh
+                assert cs + 0 - r <= jl and cs + ks * P - 1 - r >= jh
 
 
 def brute_sw(A, B, ma, mi, go, ge):
