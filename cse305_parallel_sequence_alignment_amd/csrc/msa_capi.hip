@@ -12,6 +12,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <map>
 #include <vector>
 
 #include "../../include/msa.h"
@@ -120,6 +121,10 @@ struct msa_plan {
   msa_stripe_meta* d_meta = nullptr;
   int* d_ticket = nullptr;  // [0] ticket, [1] err
   unsigned long long* d_gbuf = nullptr;
+  uint8_t* d_cod = nullptr;                // MSA_NCOPY byte-shifted padded column-code copies
+  msa_pair_desc* d_segs = nullptr;         // distinct column sequences (b_off, n, cod_off)
+  std::vector<msa_pair_desc> segs;
+  int64_t cod_copy = 0;                    // bytes per copy
   PairResult* d_res = nullptr;
   unsigned long long* d_sum = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -198,13 +203,19 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     default: delete P; return MSA_ERR_ARG;
   }
   const int tp = (kalg == MSA_ALG_SWL || kalg == MSA_ALG_SWA) ? (desc->track_end ? 1 : 0) : 0;
-  const int W = desc->single ? MSA_WAVES_SINGLE : MSA_WAVES_BATCH;
+  if (desc->single && desc->n_pairs != 1) { delete P; return MSA_ERR_ARG; }
+  // A banded pair has only ~(2*band+64)/(64*lag) stripes in flight at once:
+  // one workgroup cycling its waves over all stripes (the batch kernel, wrap
+  // link through the LDS row buffer) beats a chain of cross-workgroup hand-offs.
+  bool single = desc->single != 0;
+  if (single && kalg == MSA_ALG_NWA && desc->band >= 0 && (int64_t)desc->band * 2 + 64 < desc->n[0] / 4) single = false;
+  P->d.single = single ? 1 : 0;
+  const int W = single ? MSA_WAVES_SINGLE : MSA_WAVES_BATCH;
   P->W = W;
-  const int KS = desc->single ? MSA_KS_SINGLE : MSA_KS_BATCH;
+  const int KS = single ? MSA_KS_SINGLE : MSA_KS_BATCH;
   P->KS = KS;
   P->fn = pick_kernel(kalg, out_mode, tp, W);
   if (!P->fn) { delete P; return MSA_ERR_UNSUPPORTED; }
-  if (desc->single && desc->n_pairs != 1) { delete P; return MSA_ERR_ARG; }
   P->nc = nc_of(kalg);
   const int band = (kalg == MSA_ALG_NWA) ? desc->band : -1;
   msa_kparams& kp = P->kp;
@@ -219,12 +230,13 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   kp.h = desc->gap_open - desc->gap_extend;
   kp.start_type = desc->start_type;
   kp.band = band;
-  kp.single = desc->single ? 1 : 0;
+  kp.single = single ? 1 : 0;
   kp.n_pairs = (int)desc->n_pairs;
   if (kalg == MSA_ALG_NWA && kp.h < 0) { delete P; return MSA_ERR_UNSUPPORTED; }
   // geometry
-  int64_t stripe0 = 0, off = 0;
-  int max_S = 0, max_P = 0, max_code = 0;
+  int64_t stripe0 = 0, off = 0, cod_bytes = 0;
+  std::map<std::pair<int64_t, int64_t>, int64_t> seg_of;
+  int max_S = 0, max_P = 0;
   P->pairs.resize(desc->n_pairs);
   for (int64_t p = 0; p < desc->n_pairs; ++p) {
     const int64_t m = desc->m[p], n = desc->n[p];
@@ -242,19 +254,10 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     if (band >= 0 && std::llabs(m - n) > band) { delete P; return MSA_ERR_ARG; }
     const int S = (int)((m + 63) / 64);
     int pmax = 0;
-    // per-item code window (items = groups of W stripes in single mode, whole pair in batch)
-    const int per_item = desc->single ? W : S;
-    for (int k0 = 0; k0 < S; k0 += per_item) {
-      int cmin = 1 << 30, cmax = -(1 << 30);
-      for (int k = k0; k < std::min(S, k0 + per_item); ++k) {
-        StripeGeom g;
-        stripe_geom(k, (int)m, (int)n, band, g, KS);
-        pmax = std::max(pmax, g.P * (KS / MSA_K));  // in 16-step layout blocks
-        cmin = std::min(cmin, g.cs - 64);
-        cmax = std::max(cmax, g.cs + g.P * KS);
-      }
-      cmin &= ~3;
-      max_code = std::max(max_code, cmax - cmin + 8);
+    for (int k = 0; k < S; ++k) {
+      StripeGeom g;
+      stripe_geom(k, (int)m, (int)n, band, g, KS);
+      pmax = std::max(pmax, g.P * (KS / MSA_K));  // in 16-step layout blocks
     }
     msa_pair_desc& pd = P->pairs[p];
     pd.a_off = desc->a_off[p];
@@ -264,6 +267,21 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     pd.stripe0 = (int)stripe0;
     pd.pmax = pmax;
     pd.out_off = off;
+    // padded column-code segment, shared by pairs with the same column sequence
+    {
+      const auto key = std::make_pair(pd.b_off, (int64_t)n);
+      auto it = seg_of.find(key);
+      if (it == seg_of.end()) {
+        it = seg_of.emplace(key, cod_bytes).first;
+        msa_pair_desc sd{};
+        sd.b_off = pd.b_off;
+        sd.n = (int)n;
+        sd.cod_off = cod_bytes;
+        P->segs.push_back(sd);
+        cod_bytes += ((n + 2 * MSA_CPAD) + 63) & ~int64_t(63);
+      }
+      pd.cod_off = it->second;
+    }
     const int64_t cells = (int64_t)S * pmax * MSA_K * 64;
     off += (cells + 63) & ~int64_t(63);
     stripe0 += S;
@@ -272,17 +290,18 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   }
   P->total_stripes = stripe0;
   P->cells_elems = off;
-  kp.sched_cap = desc->single ? W : max_S;
-  kp.lds_code_bytes = ((max_code + 48) + 15) & ~15;  // + slack: the prefetch of phase P reads past the window
-  kp.lds_row_words = desc->single ? 0 : (((max_P * MSA_K + MSA_ROWOFF + 32) + 15) & ~15);
-  if (desc->single) {
+  kp.sched_cap = single ? W : max_S;
+  kp.lds_code_bytes = 0;  // column codes come from the staged global copies (stage_codes_kernel)
+  P->cod_copy = cod_bytes;
+  kp.lds_row_words = single ? 0 : (((max_P * MSA_K + MSA_ROWOFF + 32) + 15) & ~15);
+  if (single) {
     const int S = (int)((desc->m[0] + 63) / 64);
     kp.n_items = (S + W - 1) / W;
   } else {
     kp.n_items = (int)desc->n_pairs;
   }
   const size_t lds_ints = 16 + (size_t)kp.sched_cap * 8 + (size_t)(2 * W + 1) * P->nc * MSA_RING +
-                          (size_t)P->nc * kp.lds_row_words + (size_t)kp.lds_code_bytes;  // 4 copies = bytes*4/4
+                          (size_t)P->nc * kp.lds_row_words;
   P->lds_bytes = lds_ints * 4;
   if (P->lds_bytes > 160 * 1024) {
     std::fprintf(stderr, "msa: problem needs %zu B of LDS per workgroup (> 160 KiB)\n", P->lds_bytes);
@@ -314,9 +333,14 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   if (hipMemset(P->d_meta, 0, sizeof(msa_stripe_meta) * std::max<int64_t>(1, P->total_stripes)) != hipSuccess)
     return fail();
   if (hipMalloc(&P->d_ticket, 64) != hipSuccess) return fail();
+  if (hipMalloc(&P->d_cod, (size_t)MSA_NCOPY * P->cod_copy + 64) != hipSuccess) return fail();
+  if (hipMalloc(&P->d_segs, sizeof(msa_pair_desc) * P->segs.size()) != hipSuccess) return fail();
+  if (hipMemcpy(P->d_segs, P->segs.data(), sizeof(msa_pair_desc) * P->segs.size(), hipMemcpyHostToDevice) !=
+      hipSuccess)
+    return fail();
   if (hipMalloc(&P->d_res, sizeof(PairResult) * desc->n_pairs) != hipSuccess) return fail();
   if (hipMalloc(&P->d_sum, 64) != hipSuccess) return fail();
-  if (desc->single && kp.n_items > 1) {
+  if (single && kp.n_items > 1) {
     P->gbuf_stride = (int)(((desc->n[0] + 2 * MSA_GOFF + 16) + 15) & ~15);
     const size_t gb = (size_t)(kp.n_items - 1) * P->nc * P->gbuf_stride * sizeof(unsigned long long);
     if (hipMalloc(&P->d_gbuf, gb) != hipSuccess) return fail();
@@ -333,6 +357,8 @@ void msa_plan_destroy(msa_plan* P) {
   if (P->d_meta) (void)hipFree(P->d_meta);
   if (P->d_ticket) (void)hipFree(P->d_ticket);
   if (P->d_gbuf) (void)hipFree(P->d_gbuf);
+  if (P->d_cod) (void)hipFree(P->d_cod);
+  if (P->d_segs) (void)hipFree(P->d_segs);
   if (P->d_res) (void)hipFree(P->d_res);
   if (P->d_sum) (void)hipFree(P->d_sum);
   if (P->ev0) (void)hipEventDestroy(P->ev0);
@@ -381,7 +407,15 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
   a.outT2 = (int32_t*)c1;
   a.outT3 = (int32_t*)c2;
   a.stamps = P->stamps;
+  a.cod = P->d_cod;
+  a.cod_copy = P->cod_copy;
   HIPCHK(hipMemsetAsync(P->d_ticket, 0, 64, st));
+  {
+    const unsigned virt = (P->kp.alg == MSA_ALG_SWL || P->kp.alg == MSA_ALG_SWA) ? MSA_VIRT_CODE : 0u;
+    hipLaunchKernelGGL(stage_codes_kernel, dim3(64, (unsigned)P->segs.size()), dim3(256), 0, st, dB, P->d_segs,
+                       (int)P->segs.size(), P->d_cod, (long long)P->cod_copy, virt);
+    HIPCHK(hipGetLastError());
+  }
   HIPCHK(hipEventRecord(P->ev0, st));
   hipLaunchKernelGGL(P->fn, dim3(P->grid), dim3((P->W + 1) * 64), P->lds_bytes, st, a);
   HIPCHK(hipGetLastError());

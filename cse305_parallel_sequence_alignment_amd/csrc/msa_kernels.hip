@@ -53,6 +53,8 @@
 #define MSA_GOFF 128
 #define MSA_NEG (-(1 << 30))
 #define MSA_VIRT_CODE 7u     // SW: column code outside [1, n] (real symbols use codes 0..6)
+#define MSA_CPAD 256         // code segment padding (bytes) on each side of a pair's columns
+#define MSA_NCOPY 16         // byte-shifted code copies: every lane reads 16-byte aligned dwordx4
 #define MSA_VIRT_SCORE (-100)  // its profile byte (s + 2g space for SWL; < 0 is all that matters)
 
 namespace msa {
@@ -126,6 +128,8 @@ struct KArgs {
   int32_t* outT2;            // O_TAB planes
   int32_t* outT3;
   uint8_t* outDir;           // O_DIR
+  const uint8_t* cod;        // MSA_NCOPY byte-shifted copies of the padded column codes (stage_codes_kernel)
+  long long cod_copy;        // bytes per copy
   unsigned long long* stamps;  // diagnostic build only (MSA_STAMPS): per-phase s_memtime
 };
 
@@ -209,8 +213,6 @@ struct LaneState {
   int fin[3];
   unsigned plo, phi;  // substitution profile (8 int8 scores by column code)
   int i;              // DP row
-  int cw_base;        // LDS dword index base of this lane's code stream (copy cw_copy)
-  int cw_copy;
 };
 
 // One DP step for every lane.  in[v] = value lane 0 takes from the row above.
@@ -443,8 +445,6 @@ __global__ __launch_bounds__((W + 1) * 64) void stripe_kernel(KArgs a) {
   int* rings = smem + 16 + sched_cap * 8;
   int* stage = rings + 2 * W * NC * MSA_RING;
   int* rowbuf = stage + NC * MSA_RING;  // NC x lds_row_words (batch wrap link)
-  unsigned* codes = reinterpret_cast<unsigned*>(rowbuf + NC * kp.lds_row_words);  // 4 copies
-  const int code_dwords = kp.lds_code_bytes / 4;
 
   for (;;) {
     // ---- ticket ----
@@ -475,7 +475,6 @@ __global__ __launch_bounds__((W + 1) * 64) void stripe_kernel(KArgs a) {
     // ---- schedule (one lane) ----
     if (threadIdx.x == 0) {
       int total = 0;
-      int cmin = 1 << 30, cmax = -(1 << 30);
       StripeGeom prev;
       for (int k = 0; k < ns; ++k) {
         StripeGeom g;
@@ -496,35 +495,12 @@ __global__ __launch_bounds__((W + 1) * 64) void stripe_kernel(KArgs a) {
         sched[k] = g;
         prev = g;
         total = max(total, T + g.P);
-        cmin = min(cmin, g.cs - 64);
-        cmax = max(cmax, g.cs + g.P * KS);
       }
       misc[1] = total;
-      misc[2] = cmin & ~3;  // code window base column (multiple of 4)
-      misc[3] = cmax;
     }
     __syncthreads();
     const int total = uni(misc[1]);
-    const int cbase = uni(misc[2]);
-    const int cwin = uni(misc[3]) - cbase + 8;  // bytes needed per copy
 
-    // ---- column codes -> 4 byte-shifted LDS copies ----
-    {
-      const uint8_t* Bp = a.B + pd.b_off;
-      const int nd = min((cwin + 3) / 4, code_dwords);
-      for (int idx = threadIdx.x; idx < 4 * nd; idx += blockDim.x) {
-        const int cp = idx / nd, d = idx - cp * nd;
-        unsigned word = 0;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          const int col = cbase + 4 * d + cp + b;
-          const unsigned code = (col >= 1 && col <= n) ? (unsigned)Bp[col - 1] : (SWK ? MSA_VIRT_CODE : 0u);
-          word |= (code & 7u) << (8 * b);
-        }
-        codes[cp * code_dwords + d] = word;
-      }
-    }
-    __syncthreads();
     const unsigned ep = kp.epoch;
 
     if (w == W) {
@@ -694,12 +670,24 @@ __global__ __launch_bounds__((W + 1) * 64) void stripe_kernel(KArgs a) {
         L.plo = lo;
         L.phi = hi;
       }
-      // code stream: lane reads bytes starting at column cs - lane
+      // code stream: lane r needs columns cs - r + t; column c sits in copy
+      // (c-1+CPAD)&15 at byte (c-1+CPAD) & ~15, so every read is an aligned dwordx4
+      const unsigned* cptr;
       {
-        const int b0 = sg.cs - lane - cbase;  // >= 1 by construction
-        L.cw_copy = b0 & 3;
-        L.cw_base = L.cw_copy * code_dwords + (b0 >> 2);
+        const int b0 = sg.cs - lane - 1 + MSA_CPAD;  // > 0
+        cptr = reinterpret_cast<const unsigned*>(a.cod + (size_t)(b0 & (MSA_NCOPY - 1)) * a.cod_copy + pd.cod_off +
+                                                 (b0 & ~(MSA_NCOPY - 1)));
       }
+      // codes of phase q+1 are loaded during phase q (global loads, latency hidden)
+      unsigned cwn[KS / 4];
+      auto load_codes = [&](const int q) {
+#pragma unroll
+        for (int u = 0; u < KS / 4; u += 4) {
+          const uint4 c4 = *reinterpret_cast<const uint4*>(cptr + (KS / 4) * q + u);
+          cwn[u] = c4.x; cwn[u + 1] = c4.y; cwn[u + 2] = c4.z; cwn[u + 3] = c4.w;
+        }
+      };
+      load_codes(0);
       // input: the loader's staging ring (row 0 or the previous workgroup),
       // the wrap row buffer (batch), or the ring of the previous wave
       const int* in_ptr;
@@ -769,17 +757,9 @@ __global__ __launch_bounds__((W + 1) * 64) void stripe_kernel(KArgs a) {
           }
         }
         unsigned cw[KS / 4];
-        {
-          const unsigned* cp = codes + L.cw_base + (KS / 4) * q;  // per-lane, dword aligned only
 #pragma unroll
-          for (int u = 0; u < KS / 4; ++u) {
-#ifdef MSA_DBG_NO_CW
-            cw[u] = (unsigned)(L.cw_base + q * 0x01010101 + u);
-#else
-            cw[u] = cp[u];
-#endif
-          }
-        }
+        for (int u = 0; u < KS / 4; ++u) cw[u] = cwn[u];
+        load_codes(q + 1);
         int hist[NC][KS];
         int hv[KS];
         unsigned dirw[KS / 4];
@@ -936,6 +916,29 @@ __global__ __launch_bounds__((W + 1) * 64) void stripe_kernel(KArgs a) {
       }
     }
     for (; ph < total; ++ph) MSA_SYNC(ph);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Column codes -> MSA_NCOPY byte-shifted, padded copies (one thread per output dword):
+// copy c, byte x of pair p = code of column x + c - CPAD + 1 (virt outside [1, n]).
+// ---------------------------------------------------------------------------
+__global__ void stage_codes_kernel(const uint8_t* B, const msa_pair_desc* pairs, int n_pairs, uint8_t* cod,
+                                   long long cod_copy, unsigned virt) {
+  const int p = blockIdx.y;
+  if (p >= n_pairs) return;
+  const msa_pair_desc pd = pairs[p];
+  const int seg = ((pd.n + 2 * MSA_CPAD) + 15) & ~15;  // bytes per copy of this pair (multiple of 16)
+  for (int d = blockIdx.x * blockDim.x + threadIdx.x; d < MSA_NCOPY * (seg / 4); d += gridDim.x * blockDim.x) {
+    const int c = d / (seg / 4), x = 4 * (d - c * (seg / 4));
+    unsigned word = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int col = x + b + c - MSA_CPAD + 1;
+      const unsigned code = (col >= 1 && col <= pd.n) ? (B[pd.b_off + col - 1] & 7u) : virt;
+      word |= code << (8 * b);
+    }
+    *reinterpret_cast<unsigned*>(cod + (size_t)c * cod_copy + pd.cod_off + x) = word;
   }
 }
 

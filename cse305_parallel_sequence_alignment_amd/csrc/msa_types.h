@@ -32,6 +32,7 @@ typedef struct msa_pair_desc {
   int32_t stripe0;     // first global stripe index of this pair (result / meta arrays)
   int32_t pmax;        // phases reserved per stripe in the output layout
   int64_t out_off;     // element offset of this pair's output block
+  int64_t cod_off;     // byte offset of this pair's padded column-code segment in each code copy
 } msa_pair_desc;
 
 // Per-stripe metadata written by the kernel (host uses it to de-skew).

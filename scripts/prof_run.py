@@ -1,7 +1,11 @@
-"""Minimal driver for rocprofv3 runs: a few launches of one workload."""
-import sys, os
+"""Minimal driver for rocprofv3 runs: a few launches of one bench workload (same plans as bench.py)."""
+import os
+import sys
+
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import numpy as np, torch
+import numpy as np
+import torch
+
 from cse305_parallel_sequence_alignment_amd import _lib as LB
 from cse305_parallel_sequence_alignment_amd.plan import Plan
 from oracle.oracle import load_dataset
@@ -9,22 +13,27 @@ from oracle.oracle import load_dataset
 wl = sys.argv[1] if len(sys.argv) > 1 else "c2"
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 seqs = load_dataset()[1]
-enc = lambda s: torch.from_numpy(np.frombuffer(s.translate(bytes.maketrans(b"ACGT", b"\x00\x01\x02\x03")), dtype=np.uint8).copy()).cuda()
-if wl == "c2n":
+enc = lambda s: torch.from_numpy(np.frombuffer(s.translate(bytes.maketrans(b"ACGT", b"\x00\x01\x02\x03")),
+                                               dtype=np.uint8).copy()).cuda()
+out = None
+if wl in ("c2", "c2n"):
     A, B = seqs[1][:10000], seqs[0][:10000]
-    pl = Plan(LB.SW_LINEAR, LB.CELLS_NONE, [10000], [10000], [0], [0], match=1, mismatch=0, gap_open=1, gap_extend=1)
-    out = None
-elif wl == "c2":
-    A, B = seqs[1][:10000], seqs[0][:10000]
-    pl = Plan(LB.SW_LINEAR, LB.CELLS_H, [10000], [10000], [0], [0], match=1, mismatch=0, gap_open=1, gap_extend=1)
-    out = torch.empty(pl.cells_elems, dtype=torch.int32, device="cuda")
-else:
+    cells = LB.CELLS_H if wl == "c2" else LB.CELLS_NONE
+    pl = Plan(LB.SW_LINEAR, cells, [10000], [10000], [0], [0], match=1, mismatch=0, gap_open=1, gap_extend=1)
+elif wl == "c5":
+    A, B = (seqs[4] * 3)[:20000], (seqs[5] * 3)[:20000]
+    pl = Plan(LB.SW_AFFINE, LB.CELLS_DIR, [20000], [20000], [0], [0], match=1, mismatch=0, gap_open=3,
+              gap_extend=1, track_end=True)
+else:  # c4
     L, K = 4000, 1024
     rng = np.random.default_rng(0x5EED0004)
     offs = rng.integers(0, 13309 - L, size=K)
-    A = b"".join(seqs[k % 20][offs[k]:offs[k] + L] for k in range(K)); B = seqs[0][:L]
-    pl = Plan(LB.SW_LINEAR, LB.CELLS_NONE, [L] * K, [L] * K, [k * L for k in range(K)], [0] * K, match=1, mismatch=0, gap_open=1, gap_extend=1)
-    out = None
+    A = b"".join(seqs[k % 20][offs[k]:offs[k] + L] for k in range(K))
+    B = seqs[0][:L]
+    pl = Plan(LB.SW_LINEAR, LB.CELLS_NONE, [L] * K, [L] * K, [k * L for k in range(K)], [0] * K, match=1,
+              mismatch=0, gap_open=1, gap_extend=1)
+if pl.cells != LB.CELLS_NONE:
+    out = torch.empty(pl.cells_elems, dtype=torch.uint8 if pl.cells == LB.CELLS_DIR else torch.int32, device="cuda")
 dA, dB = enc(A), enc(B)
 for _ in range(reps):
     pl.run(dA, dB, out)
