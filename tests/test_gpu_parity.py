@@ -218,3 +218,29 @@ def test_nw_banded_reference_gotoh(oracle, dev, LB, m, n, w):
     assert np.array_equal(Hd[inb], Ho[inb])
     assert pl.checksum(H) == oracle.checksum_h(Ho, w)
     assert pl.results()[0]["score"] == int(score)
+
+
+def test_reference_harness_linked_against_compat(tmp_path):
+    """The reference's own harness (main.cpp + testing.cpp + pull_data.cpp, unmodified, built by
+    oracle/Makefile into oracle/_ref/harness_msa) linked against libmsa_compat.so instead of the
+    reference's alignment objects: its stdout alignment equals the reference's (golden md5)."""
+    import gzip
+    import shutil
+    import subprocess
+
+    from conftest import ROOT
+
+    exe = ROOT / "oracle" / "_ref" / "harness_msa"
+    if not exe.exists():
+        pytest.skip("oracle/_ref/harness_msa not built (reference sources absent at build time)")
+    with gzip.open(GOLDEN / "gene_sequences_test.gz", "rb") as f, open(tmp_path / "gene_sequences_test", "wb") as o:
+        shutil.copyfileobj(f, o)
+    r = subprocess.run([str(exe)], cwd=tmp_path, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = r.stdout.split("\n")
+    assert "Finished threads" in lines
+    i = lines.index("bp1")
+    block = "\n".join(lines[i:i + 7]) + "\n"
+    kat = json.loads((GOLDEN / "kat.json").read_text())
+    want = [h for h in kat["harness"] if (h["a"], h["b"], h["L"]) == (2, 15, 50)][0]
+    assert hashlib.md5(block.encode()).hexdigest() == want["stdout_md5"], block

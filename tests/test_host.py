@@ -136,3 +136,12 @@ def test_banded_equals_full_when_band_covers(oracle):
         B = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), n).tobytes()
         _, full = oracle.main_alignment_text(A, B, 1.0, 2.0)
         assert oracle.banded_ref(A, B, max(m, n) + 2, 1.0, 2.0) == full
+
+
+def test_compat_library_exports_reference_symbol():
+    """libmsa_compat.so exports main_alignment_function with the reference's C++ mangling
+    (alignment_algorithm/main_alignment.h:38 -> _Z23main_alignment_functionPcS_mmmdd)."""
+    lib = ROOT / "cse305_parallel_sequence_alignment_amd" / "libmsa_compat.so"
+    assert lib.exists(), "build libmsa_compat.so (make -C cse305_parallel_sequence_alignment_amd/csrc)"
+    L = C.CDLL(str(lib))
+    assert hasattr(L, "_Z23main_alignment_functionPcS_mmmdd")
