@@ -301,7 +301,8 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     kp.n_items = (int)desc->n_pairs;
   }
   const size_t lds_ints = 16 + (size_t)kp.sched_cap * 8 + (size_t)(2 * W + 1) * P->nc * MSA_RING +
-                          (size_t)P->nc * kp.lds_row_words;
+                          (size_t)P->nc * kp.lds_row_words +
+                          (single && MSA_KS_SINGLE > 16 ? (size_t)4 * (MSA_CRING / 4 + 16) : 0);  // code ring
   P->lds_bytes = lds_ints * 4;
   if (P->lds_bytes > 160 * 1024) {
     std::fprintf(stderr, "msa: problem needs %zu B of LDS per workgroup (> 160 KiB)\n", P->lds_bytes);
@@ -314,7 +315,8 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     return MSA_ERR_HIP;
   }
   int occ = 1;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)P->fn, (W + 1) * 64, P->lds_bytes) != hipSuccess || occ < 1)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)P->fn, (W + 1 + (KS > 16 ? 1 : 0)) * 64,
+                                                   P->lds_bytes) != hipSuccess || occ < 1)
     occ = 1;
   hipDeviceProp_t prop;
   int dev = 0;
@@ -417,7 +419,8 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipEventRecord(P->ev0, st));
-  hipLaunchKernelGGL(P->fn, dim3(P->grid), dim3((P->W + 1) * 64), P->lds_bytes, st, a);
+  const int waves = P->W + 1 + (P->KS > 16 ? 1 : 0);  // compute + loader (+ code wave, single pair)
+  hipLaunchKernelGGL(P->fn, dim3(P->grid), dim3(waves * 64), P->lds_bytes, st, a);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(P->ev1, st));
   const int sw = (P->kp.alg == MSA_ALG_SWL || P->kp.alg == MSA_ALG_SWA) ? 1 : 0;

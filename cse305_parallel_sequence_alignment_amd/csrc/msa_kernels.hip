@@ -55,6 +55,7 @@
 #define MSA_VIRT_CODE 7u     // SW: column code outside [1, n] (real symbols use codes 0..6)
 #define MSA_CPAD 256         // code segment padding (bytes) on each side of a pair's columns
 #define MSA_NCOPY 16         // byte-shifted code copies: every lane reads 16-byte aligned dwordx4
+#define MSA_CRING 1024       // single-pair LDS code ring: columns per copy (+64 B mirror), 4 copies
 #define MSA_VIRT_SCORE (-100)  // its profile byte (s + 2g space for SWL; < 0 is all that matters)
 
 namespace msa {
@@ -364,7 +365,9 @@ enum Snk { SNK_NONE = 0, SNK_RING = 1, SNK_ROW = 2, SNK_GLOBAL = 3 };
 // ever waits on a global load.  Prefetch slots are compile-time indices
 // (loop unrolled by MSA_LOAD_AHEAD): no register rotation, hence no forced
 // vmcnt(0) right after a load.
-#define MSA_LOAD_AHEAD 4
+#ifndef MSA_LOAD_AHEAD
+#define MSA_LOAD_AHEAD 2
+#endif
 
 // Phase barrier.  The diagnostic build (-DMSA_STAMPS) records s_memtime just
 // before and after every barrier of every wave: stamps[((item*16 + wave)*4096
@@ -423,7 +426,7 @@ __device__ __forceinline__ unsigned long long loader_issue(const KArgs& a, int c
 }
 
 template <int ALG, int OUT, bool TRACKPOS, int W, int KS>
-__global__ __launch_bounds__((W + 1) * 64) void stripe_kernel(KArgs a) {
+__global__ __launch_bounds__((W + 1 + (KS > 16 ? 1 : 0)) * 64) void stripe_kernel(KArgs a) {
   static_assert(KS % 16 == 0 && KS <= 64, "phases are whole 16-step layout blocks");
   constexpr int CPP = KS / 16;  // 16-column chunks per phase
   constexpr int NC = Tr<ALG>::NC;
@@ -445,6 +448,14 @@ __global__ __launch_bounds__((W + 1) * 64) void stripe_kernel(KArgs a) {
   int* rings = smem + 16 + sched_cap * 8;
   int* stage = rings + 2 * W * NC * MSA_RING;
   int* rowbuf = stage + NC * MSA_RING;  // NC x lds_row_words (batch wrap link)
+  // single pair: 4 byte-shifted copies of a sliding column-code window, staged
+  // by the loader wave two phases ahead, so compute waves never wait on vmcnt
+  // (their only VMEM ops are stores).  Copy c, dword d holds columns
+  // 4D+c..4D+c+3 for the live D = d (mod MSA_CRING/4); dwords [RING/4, RING/4+16)
+  // mirror [0, 16) so a phase's KS/4 consecutive dwords never wrap.
+  constexpr bool LDSCODE = (KS > 16);
+  constexpr int CRW = MSA_CRING / 4 + 16;  // dwords per copy
+  unsigned* cring = reinterpret_cast<unsigned*>(rowbuf + NC * kp.lds_row_words);
 
   for (;;) {
     // ---- ticket ----
@@ -502,6 +513,89 @@ __global__ __launch_bounds__((W + 1) * 64) void stripe_kernel(KArgs a) {
     const int total = uni(misc[1]);
 
     const unsigned ep = kp.epoch;
+
+    if (LDSCODE && w == W + 1) {
+      // =================== code wave (single pair) ===================
+      const StripeGeom s0 = sched[0];
+      // ---- column-code ring (single pair): columns needed at phase x = union over
+      // the item's stripes active at x of [cs + KS(x-T) - 63, cs + KS(x-T) + KS + 3]
+      auto need_hi = [&](int x) {
+        int hi = INT32_MIN;
+        for (int k = 0; k < ns; ++k) {
+          const int T = sched[k].T, P_ = sched[k].P, c0 = sched[k].cs;
+          if (T <= x && x < T + P_) hi = max(hi, c0 + KS * (x - T) + KS + 3);
+        }
+        return uni(hi);
+      };
+      const unsigned* cod_pair = reinterpret_cast<const unsigned*>(a.cod + pd.cod_off);
+      const int cc = lane >> 4, ck = lane & 15;  // this lane stages copy cc, dword slot ck
+      // global source of the 4 codes of columns 4D+cc..4D+cc+3 (an aligned dword of a shifted copy)
+      auto code_src = [&](int D) {
+        const int g = 4 * D + cc - 1 + MSA_CPAD;
+        return cod_pair + ((size_t)(g & (MSA_NCOPY - 1)) * a.cod_copy + (g & ~(MSA_NCOPY - 1))) / 4;
+      };
+      auto code_put = [&](int D, unsigned v) {
+        const int d = D & (MSA_CRING / 4 - 1);
+        cring[cc * CRW + d] = v;
+        if (d < 16) cring[cc * CRW + d + MSA_CRING / 4] = v;
+      };
+      // dword range of copy cc covering columns (a_, b_]
+      auto drange = [&](int a_, int b_, int& dlo, int& dhi) {
+        dlo = ((a_ + 1 - cc - 3) >> 2);
+        dhi = ((b_ - cc) >> 2);
+      };
+      int staged = 0;  // highest column staged so far (wave-uniform)
+      unsigned cval[2] = {0u, 0u};
+      int cD[2] = {0, 0};
+      bool cok[2] = {false, false};
+      if constexpr (LDSCODE) {
+        // prologue: everything phases 0 and 1 read, synchronously
+        const int lo0 = s0.cs - 63 - 4;
+        const int hi1 = max(need_hi(0), need_hi(1));
+        int dlo, dhi;
+        drange(lo0 - 1, hi1, dlo, dhi);
+        for (int D = dlo + ck; D <= dhi; D += 16) code_put(D, *code_src(D));
+        staged = hi1;
+      }
+      // issue the loads for columns needed at phase x into slot `sl`; commit later
+      auto code_issue = [&](int x, int sl) {
+        const int hi = need_hi(x);
+        int dlo, dhi;
+        drange(staged, hi, dlo, dhi);
+        if (hi > staged && dhi - dlo >= 16) {  // rare big jump: stage the excess synchronously
+          for (int D = dlo + ck; D <= dhi - 16; D += 16) code_put(D, *code_src(D));
+          dlo = dhi - 15;
+        }
+        const int D = dlo + ck;
+        cok[sl] = (hi > staged) && (D <= dhi);
+        cD[sl] = D;
+        if (cok[sl]) cval[sl] = *code_src(D);
+        staged = max(staged, hi);
+      };
+      auto code_commit = [&](int sl) {
+        if (cok[sl]) code_put(cD[sl], cval[sl]);
+      };
+
+      if constexpr (LDSCODE) {
+        code_issue(2, 0);
+        __syncthreads();  // phases 0, 1 staged before any compute wave reads them
+        for (int ph = 0; ph < total; ph += 2) {
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const int p = ph + s;
+            if (p < total) {
+              // slot s holds the loads for phase p+2 (issued two iterations ago, or
+              // in the prologue): commit them (visible after this phase's barrier),
+              // then prefetch phase p+4... p+3 into the freed slot
+              code_commit(s);
+              code_issue(p + 3, s);
+              MSA_SYNC(p);
+            }
+          }
+        }
+      }
+      continue;
+    }
 
     if (w == W) {
       // =================== loader wave ===================
@@ -596,6 +690,7 @@ __global__ __launch_bounds__((W + 1) * 64) void stripe_kernel(KArgs a) {
         for (int s = 0; s < LA; ++s) {
           const int p = ph + s;
           if (p < total) {
+
             if (act) {
               if (p + 1 < s0.P) {
 #pragma unroll
@@ -678,16 +773,26 @@ __global__ __launch_bounds__((W + 1) * 64) void stripe_kernel(KArgs a) {
         cptr = reinterpret_cast<const unsigned*>(a.cod + (size_t)(b0 & (MSA_NCOPY - 1)) * a.cod_copy + pd.cod_off +
                                                  (b0 & ~(MSA_NCOPY - 1)));
       }
-      // codes of phase q+1 are loaded during phase q (global loads, latency hidden)
+      // batch: codes of phase q+1 are loaded during phase q (global loads);
+      // single pair: read from the loader-staged LDS ring at phase start
       unsigned cwn[KS / 4];
+      const int cj0 = sg.cs - lane;                // column of this lane at step 0
+      const unsigned* cr_base = cring + (cj0 & 3) * CRW;
+      const int cd0 = cj0 >> 2;                    // floor: absolute dword index at step 0
       auto load_codes = [&](const int q) {
+        if constexpr (LDSCODE) {
+          const unsigned* cp = cr_base + ((cd0 + (KS / 4) * q) & (MSA_CRING / 4 - 1));
 #pragma unroll
-        for (int u = 0; u < KS / 4; u += 4) {
-          const uint4 c4 = *reinterpret_cast<const uint4*>(cptr + (KS / 4) * q + u);
-          cwn[u] = c4.x; cwn[u + 1] = c4.y; cwn[u + 2] = c4.z; cwn[u + 3] = c4.w;
+          for (int u = 0; u < KS / 4; ++u) cwn[u] = cp[u];
+        } else {
+#pragma unroll
+          for (int u = 0; u < KS / 4; u += 4) {
+            const uint4 c4 = *reinterpret_cast<const uint4*>(cptr + (KS / 4) * q + u);
+            cwn[u] = c4.x; cwn[u + 1] = c4.y; cwn[u + 2] = c4.z; cwn[u + 3] = c4.w;
+          }
         }
       };
-      load_codes(0);
+      if constexpr (!LDSCODE) load_codes(0);
       // input: the loader's staging ring (row 0 or the previous workgroup),
       // the wrap row buffer (batch), or the ring of the previous wave
       const int* in_ptr;
@@ -757,9 +862,26 @@ __global__ __launch_bounds__((W + 1) * 64) void stripe_kernel(KArgs a) {
           }
         }
         unsigned cw[KS / 4];
+        if constexpr (LDSCODE) load_codes(q);
 #pragma unroll
-        for (int u = 0; u < KS / 4; ++u) cw[u] = cwn[u];
-        load_codes(q + 1);
+        for (int u = 0; u < KS / 4; ++u) {
+#ifdef MSA_DBG_NO_CW
+          cw[u] = (unsigned)(lane + q * 0x01010101 + u) & 0x03030303u;
+#else
+          cw[u] = cwn[u];
+#endif
+        }
+#ifdef MSA_STAMPS
+        {
+          int z = IN[0][0] ^ (int)cw[0];
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+          asm volatile("" ::"v"(z));
+          MSA_MARK(ph + q, 3);
+        }
+#endif
+#ifndef MSA_DBG_NO_CW
+        if constexpr (!LDSCODE) load_codes(q + 1);
+#endif
         int hist[NC][KS];
         int hv[KS];
         unsigned dirw[KS / 4];
