@@ -44,7 +44,9 @@
 #ifndef MSA_WAVES_SINGLE
 #define MSA_WAVES_SINGLE 4  // single pair: one compute wave per SIMD (latency-bound wavefront)
 #endif
+#ifndef MSA_KS_SINGLE
 #define MSA_KS_SINGLE 32  // steps per phase, single pair: fewer phases amortise the per-phase sync
+#endif
 #define MSA_KS_BATCH 16   // steps per phase, batch: fewer registers, two workgroups per CU
 #define MSA_WAVES_BATCH 8   // batch: two per SIMD (throughput-bound, hides the step chain)
 #define MSA_K 16  // output layout block: cells are stored in blocks of 16 steps (any KS is a multiple)
@@ -373,20 +375,25 @@ enum Snk { SNK_NONE = 0, SNK_RING = 1, SNK_ROW = 2, SNK_GLOBAL = 3 };
 // before and after every barrier of every wave: stamps[((item*16 + wave)*4096
 // + phase)*2 + {0,1}] (phases >= 4096 and items >= 64 are not recorded).
 #ifdef MSA_STAMPS
+#ifdef MSA_STAMPS_RT
+#define MSA_CLOCK() __builtin_amdgcn_s_memrealtime()  // chip-wide 100 MHz: comparable across XCDs
+#else
+#define MSA_CLOCK() __builtin_amdgcn_s_memtime()
+#endif
 #define MSA_SYNC(ph_)                                                                       \
   do {                                                                                      \
     const int ph__ = (ph_);                                                                 \
     const bool rec__ = a.stamps && lane == 0 && ph__ < 4096 && item < 64;                   \
     const size_t o__ = (((size_t)item * 16 + w) * 4096 + ph__) * 4;                          \
-    if (rec__) a.stamps[o__] = __builtin_amdgcn_s_memtime();                                \
+    if (rec__) a.stamps[o__] = MSA_CLOCK();                                                 \
     __syncthreads();                                                                        \
-    if (rec__) a.stamps[o__ + 1] = __builtin_amdgcn_s_memtime();                            \
+    if (rec__) a.stamps[o__ + 1] = MSA_CLOCK();                                             \
   } while (0)
 #define MSA_MARK(ph_, slot_)                                                                \
   do {                                                                                      \
     const int ph__ = (ph_);                                                                 \
     if (a.stamps && lane == 0 && ph__ < 4096 && item < 64)                                  \
-      a.stamps[(((size_t)item * 16 + w) * 4096 + ph__) * 4 + (slot_)] = __builtin_amdgcn_s_memtime(); \
+      a.stamps[(((size_t)item * 16 + w) * 4096 + ph__) * 4 + (slot_)] = MSA_CLOCK();          \
   } while (0)
 #else
 #define MSA_SYNC(ph_) __syncthreads()
@@ -659,6 +666,53 @@ __global__ __launch_bounds__((W + 1 + (KS > 16 ? 1 : 0)) * 64) void stripe_kerne
 #pragma unroll
         for (int h = 0; h < CPP; ++h) commit_border(h);
       }
+#ifndef MSA_LOADER_PREFETCH
+      // Just-in-time staging: during phase p the loader issues the granule
+      // loads of phase p+1, then waits for them (one global round trip fits
+      // in a phase) and commits -- the producer only has to be one phase plus
+      // the store->load visibility ahead, instead of LA+1 phases.
+      unsigned long long G[CPP];
+      if (act) {
+        {
+          // phase 0's columns published before anything is loaded
+          const int colw = min(min(s0.cs + 16 * (CPP - 1) + 15, chi), n);
+          unsigned spins = 0;
+          while ((unsigned)(gload(g_in + colw + MSA_GOFF) >> 32) != ep) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1u << 24)) {
+              if (lane == 0) atomicExch(a.err, 1);
+              break;
+            }
+          }
+        }
+#pragma unroll
+        for (int h = 0; h < CPP; ++h) G[h] = loader_issue<NC>(a, s0.cs, h, g_in, lane);
+#pragma unroll
+        for (int h = 0; h < CPP; ++h) loader_commit<NC>(a, s0.cs, nch0, h, G[h], g_in, stage, chi, n, ep, lane);
+      }
+      __syncthreads();  // phase 0 staged before any compute wave reads it
+      for (int p = 0; p < total; ++p) {
+        if (act) {
+          if (p + 1 < s0.P) {
+#pragma unroll
+            for (int h = 0; h < CPP; ++h) G[h] = loader_issue<NC>(a, s0.cs, (p + 1) * CPP + h, g_in, lane);
+            sink_phase(p - 1 - sl.T);
+#pragma unroll
+            for (int h = 0; h < CPP; ++h)
+              loader_commit<NC>(a, s0.cs, nch0, (p + 1) * CPP + h, G[h], g_in, stage, chi, n, ep, lane);
+          } else {
+            sink_phase(p - 1 - sl.T);
+          }
+        } else {
+          if (border && p + 1 < s0.P) {
+#pragma unroll
+            for (int h = 0; h < CPP; ++h) commit_border((p + 1) * CPP + h);
+          }
+          sink_phase(p - 1 - sl.T);  // the last stripe's phase completed by the previous barrier
+        }
+        MSA_SYNC(p);
+      }
+#else
       constexpr int NS = LA * CPP;  // prefetch slots; slot c % NS holds the load of chunk c
       unsigned long long G[NS];
       if (act) {
@@ -712,6 +766,7 @@ __global__ __launch_bounds__((W + 1 + (KS > 16 ? 1 : 0)) * 64) void stripe_kerne
           }
         }
       }
+#endif
       sink_phase(total - 1 - sl.T);
       continue;
     }
@@ -840,6 +895,11 @@ __global__ __launch_bounds__((W + 1 + (KS > 16 ? 1 : 0)) * 64) void stripe_kerne
         int IN[NC][KS];
         {
           const int* base = in_ptr + ((KS * q) & in_mask);
+#ifdef MSA_IN_LANE0
+          // only lane 0 consumes the row above (DPP old operand): read it with
+          // one active lane so the LDS returns 16 B instead of 1 KiB per read
+          if (lane == 0) {
+#endif
 #pragma unroll
           for (int v = 0; v < NC; ++v) {
 #pragma unroll
@@ -852,6 +912,9 @@ __global__ __launch_bounds__((W + 1 + (KS > 16 ? 1 : 0)) * 64) void stripe_kerne
               IN[v][4 * u + 0] = x.x; IN[v][4 * u + 1] = x.y; IN[v][4 * u + 2] = x.z; IN[v][4 * u + 3] = x.w;
             }
           }
+#ifdef MSA_IN_LANE0
+          }
+#endif
           if constexpr (INMASK) {
 #pragma unroll
             for (int k = 0; k < KS; ++k) {
