@@ -65,14 +65,14 @@ int nc_of(int alg) {
 typedef void (*kfn_t)(KArgs);
 
 template <int ALG, int OUT, bool TP>
-kfn_t kf(int W) {
+kfn_t kf(bool sgl) {
   // single pair: (MSA_WAVES_SINGLE waves, MSA_KS_SINGLE steps/phase); batch: (MSA_WAVES_BATCH, MSA_KS_BATCH)
-  return W == MSA_WAVES_SINGLE ? stripe_kernel<ALG, OUT, TP, MSA_WAVES_SINGLE, MSA_KS_SINGLE>
-                               : stripe_kernel<ALG, OUT, TP, MSA_WAVES_BATCH, MSA_KS_BATCH>;
+  return sgl ? stripe_kernel<ALG, OUT, TP, MSA_WAVES_SINGLE, MSA_KS_SINGLE, true>
+                               : stripe_kernel<ALG, OUT, TP, MSA_WAVES_BATCH, MSA_KS_BATCH, false>;
 }
 
-kfn_t pick_kernel(int alg, int out, int tp, int W) {
-#define K3(A, O) return tp ? kf<A, O, true>(W) : kf<A, O, false>(W)
+kfn_t pick_kernel(int alg, int out, int tp, bool sgl) {
+#define K3(A, O) return tp ? kf<A, O, true>(sgl) : kf<A, O, false>(sgl)
   switch (alg) {
     case MSA_ALG_SWL:
       if (out == MSA_OUT_NONE) K3(MSA_ALG_SWL, MSA_OUT_NONE);
@@ -84,17 +84,17 @@ kfn_t pick_kernel(int alg, int out, int tp, int W) {
       if (out == MSA_OUT_DIR) K3(MSA_ALG_SWA, MSA_OUT_DIR);
       break;
     case MSA_ALG_NWA:
-      if (out == MSA_OUT_NONE) return kf<MSA_ALG_NWA, MSA_OUT_NONE, false>(W);
-      if (out == MSA_OUT_H) return kf<MSA_ALG_NWA, MSA_OUT_H, false>(W);
+      if (out == MSA_OUT_NONE) return kf<MSA_ALG_NWA, MSA_OUT_NONE, false>(sgl);
+      if (out == MSA_OUT_H) return kf<MSA_ALG_NWA, MSA_OUT_H, false>(sgl);
       break;
     case MSA_ALG_REF:
-      if (out == MSA_OUT_NONE) return kf<MSA_ALG_REF, MSA_OUT_NONE, false>(W);
-      if (out == MSA_OUT_TAB) return kf<MSA_ALG_REF, MSA_OUT_TAB, false>(W);
-      if (out == MSA_OUT_DIR) return kf<MSA_ALG_REF, MSA_OUT_DIR, false>(W);
-      if (out == MSA_OUT_H) return kf<MSA_ALG_REF, MSA_OUT_H, false>(W);
+      if (out == MSA_OUT_NONE) return kf<MSA_ALG_REF, MSA_OUT_NONE, false>(sgl);
+      if (out == MSA_OUT_TAB) return kf<MSA_ALG_REF, MSA_OUT_TAB, false>(sgl);
+      if (out == MSA_OUT_DIR) return kf<MSA_ALG_REF, MSA_OUT_DIR, false>(sgl);
+      if (out == MSA_OUT_H) return kf<MSA_ALG_REF, MSA_OUT_H, false>(sgl);
       break;
     case MSA_ALG_PART:
-      if (out == MSA_OUT_TAB) return kf<MSA_ALG_PART, MSA_OUT_TAB, false>(W);
+      if (out == MSA_OUT_TAB) return kf<MSA_ALG_PART, MSA_OUT_TAB, false>(sgl);
       break;
   }
 #undef K3
@@ -214,7 +214,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   P->W = W;
   const int KS = single ? MSA_KS_SINGLE : MSA_KS_BATCH;
   P->KS = KS;
-  P->fn = pick_kernel(kalg, out_mode, tp, W);
+  P->fn = pick_kernel(kalg, out_mode, tp, single);
   if (!P->fn) { delete P; return MSA_ERR_UNSUPPORTED; }
   P->nc = nc_of(kalg);
   const int band = (kalg == MSA_ALG_NWA) ? desc->band : -1;
@@ -302,7 +302,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   }
   const size_t lds_ints = 16 + (size_t)kp.sched_cap * 8 + (size_t)(2 * W + 1) * P->nc * MSA_RING +
                           (size_t)P->nc * kp.lds_row_words +
-                          (single && MSA_KS_SINGLE > 16 ? (size_t)4 * (MSA_CRING / 4 + 16) : 0);  // code ring
+                          (single ? (size_t)4 * (MSA_CRING / 4 + 16) : 0);  // code ring
   P->lds_bytes = lds_ints * 4;
   if (P->lds_bytes > 160 * 1024) {
     std::fprintf(stderr, "msa: problem needs %zu B of LDS per workgroup (> 160 KiB)\n", P->lds_bytes);
@@ -315,7 +315,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     return MSA_ERR_HIP;
   }
   int occ = 1;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)P->fn, (W + 1 + (KS > 16 ? 1 : 0)) * 64,
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)P->fn, (W + 1 + (single ? 1 : 0)) * 64,
                                                    P->lds_bytes) != hipSuccess || occ < 1)
     occ = 1;
   hipDeviceProp_t prop;
@@ -419,7 +419,7 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipEventRecord(P->ev0, st));
-  const int waves = P->W + 1 + (P->KS > 16 ? 1 : 0);  // compute + loader (+ code wave, single pair)
+  const int waves = P->W + 1 + (P->d.single ? 1 : 0);  // compute + loader (+ code wave, single pair)
   hipLaunchKernelGGL(P->fn, dim3(P->grid), dim3(waves * 64), P->lds_bytes, st, a);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(P->ev1, st));

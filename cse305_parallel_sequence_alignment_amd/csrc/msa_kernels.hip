@@ -432,8 +432,9 @@ __device__ __forceinline__ unsigned long long loader_issue(const KArgs& a, int c
   return gload(g_in + (size_t)v * a.gbuf_stride + col + MSA_GOFF);
 }
 
-template <int ALG, int OUT, bool TRACKPOS, int W, int KS>
-__global__ __launch_bounds__((W + 1 + (KS > 16 ? 1 : 0)) * 64) void stripe_kernel(KArgs a) {
+// SGL: single-pair variant (loader + code wave, LDS code ring, DPP shift-register hand-off)
+template <int ALG, int OUT, bool TRACKPOS, int W, int KS, bool SGL>
+__global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KArgs a) {
   static_assert(KS % 16 == 0 && KS <= 64, "phases are whole 16-step layout blocks");
   constexpr int CPP = KS / 16;  // 16-column chunks per phase
   constexpr int NC = Tr<ALG>::NC;
@@ -460,7 +461,7 @@ __global__ __launch_bounds__((W + 1 + (KS > 16 ? 1 : 0)) * 64) void stripe_kerne
   // (their only VMEM ops are stores).  Copy c, dword d holds columns
   // 4D+c..4D+c+3 for the live D = d (mod MSA_CRING/4); dwords [RING/4, RING/4+16)
   // mirror [0, 16) so a phase's KS/4 consecutive dwords never wrap.
-  constexpr bool LDSCODE = (KS > 16);
+  constexpr bool LDSCODE = SGL;
   constexpr int CRW = MSA_CRING / 4 + 16;  // dwords per copy
   unsigned* cring = reinterpret_cast<unsigned*>(rowbuf + NC * kp.lds_row_words);
 
@@ -633,7 +634,7 @@ __global__ __launch_bounds__((W + 1 + (KS > 16 ? 1 : 0)) * 64) void stripe_kerne
       // one phase later (after the barrier that completes them).
       const int sl_idx = ns - 1;
       // (with the DPP shift register the compute wave publishes itself)
-      const bool sink = kp.single && (k0 + sl_idx) < S_pair - 1 && !(NC == 1 && KS > 16);
+      const bool sink = kp.single && (k0 + sl_idx) < S_pair - 1 && !(NC == 1 && SGL);
       StripeGeom sl = sched[sl_idx];
       sl.T = uni(sl.T); sl.P = uni(sl.P); sl.cs = uni(sl.cs);
       int sl_out_cs = 0;
@@ -954,7 +955,7 @@ __global__ __launch_bounds__((W + 1 + (KS > 16 ? 1 : 0)) * 64) void stripe_kerne
         // KS/4 single-lane b128 writes that all waves issue at once.
         // (single-pair kernels only: in batch the SIMDs are saturated and the
         // extra DPP per step costs more than the lockstep writes)
-        constexpr bool SHREG = (NC == 1) && (KS > 16);
+        constexpr bool SHREG = (NC == 1) && SGL;
         int shreg = 0;
         int4* hrow = reinterpret_cast<int4*>(a.outH + obase) + (size_t)((KS / 4) * q) * 64 + lane;
         int4* t2row = reinterpret_cast<int4*>(a.outT2 + obase) + (size_t)((KS / 4) * q) * 64 + lane;
