@@ -64,10 +64,14 @@ int nc_of(int alg) {
 
 typedef void (*kfn_t)(KArgs);
 
+// single-pair phase length: 32 steps for one carried value (SW linear); 16 when
+// two or three values per cell are carried (register pressure: no spills)
+constexpr int ks_single(int alg) { return alg == MSA_ALG_SWL ? MSA_KS_SINGLE : 16; }
+
 template <int ALG, int OUT, bool TP>
 kfn_t kf(bool sgl) {
   // single pair: (MSA_WAVES_SINGLE waves, MSA_KS_SINGLE steps/phase); batch: (MSA_WAVES_BATCH, MSA_KS_BATCH)
-  return sgl ? stripe_kernel<ALG, OUT, TP, MSA_WAVES_SINGLE, MSA_KS_SINGLE, true>
+  return sgl ? stripe_kernel<ALG, OUT, TP, MSA_WAVES_SINGLE, ks_single(ALG), true>
                                : stripe_kernel<ALG, OUT, TP, MSA_WAVES_BATCH, MSA_KS_BATCH, false>;
 }
 
@@ -208,11 +212,13 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   // one workgroup cycling its waves over all stripes (the batch kernel, wrap
   // link through the LDS row buffer) beats a chain of cross-workgroup hand-offs.
   bool single = desc->single != 0;
+#ifdef MSA_BANDED_BATCH
   if (single && kalg == MSA_ALG_NWA && desc->band >= 0 && (int64_t)desc->band * 2 + 64 < desc->n[0] / 4) single = false;
+#endif
   P->d.single = single ? 1 : 0;
   const int W = single ? MSA_WAVES_SINGLE : MSA_WAVES_BATCH;
   P->W = W;
-  const int KS = single ? MSA_KS_SINGLE : MSA_KS_BATCH;
+  const int KS = single ? ks_single(kalg) : MSA_KS_BATCH;
   P->KS = KS;
   P->fn = pick_kernel(kalg, out_mode, tp, single);
   if (!P->fn) { delete P; return MSA_ERR_UNSUPPORTED; }

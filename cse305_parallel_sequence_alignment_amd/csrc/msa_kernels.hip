@@ -111,7 +111,8 @@ __host__ __device__ inline void stripe_geom(int k, int m, int n, int band, Strip
   const int tmax_max = jhi_of(ilast, n, band) - g.cs + rlast;
   g.P = tmax_max / KS + 1;  // phases of KS steps
   g.mask_lo = jlo_of(ilast, band) - g.cs + rlast;  // max over rows of tmin
-  g.mask_hi = jhi_of(i0, n, band) - g.cs;          // min over rows of tmax
+  g.mask_hi = jhi_of(i0, n, band) - g.cs - 1;      // min over rows of tmax, minus 1: every row's
+                                                   // last step (final-state capture) is in a masked phase
   g.c_hi = jhi_of(ilast, n, band);
   g.T = 0;
   g.pad = 0;
@@ -226,7 +227,7 @@ struct LaneState {
 // (the 2g is folded into the substitution profile), so the loop-carried chain
 // per step is DPP -> v_max3 instead of DPP -> max -> sub -> max3.  Rings and
 // granules carry G; H = G - g*(i+j) is only formed for the output / best.
-template <int ALG, int OUT, bool MASKED, bool TRACKPOS>
+template <int ALG, int OUT, bool MASKED, bool TRACKPOS, bool FIN = false>
 __device__ __forceinline__ unsigned step(const msa_kparams& kp, LaneState<ALG>& L, const int (&in)[3], int s,
                                          int t, int ct, int (&carry)[3], int& hout) {
   unsigned dir = 0;
@@ -317,7 +318,7 @@ __device__ __forceinline__ unsigned step(const msa_kparams& kp, LaneState<ALG>& 
           L.best = imax(L.best, hv);
         }
       }
-    } else {
+    } else if constexpr (FIN) {  // only the stripe holding row m
       if (t == L.tmax) {
 #pragma unroll
         for (int v = 0; v < 3; ++v) L.fin[v] = nS[v];
@@ -527,7 +528,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
       const StripeGeom s0 = sched[0];
       // ---- column-code ring (single pair): columns needed at phase x = union over
       // the item's stripes active at x of [cs + KS(x-T) - 63, cs + KS(x-T) + KS + 3]
-      auto need_hi = [&](int x) {
+      auto need_hi = [&](int x) __attribute__((always_inline)) {
         int hi = INT32_MIN;
         for (int k = 0; k < ns; ++k) {
           const int T = sched[k].T, P_ = sched[k].P, c0 = sched[k].cs;
@@ -538,17 +539,17 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
       const unsigned* cod_pair = reinterpret_cast<const unsigned*>(a.cod + pd.cod_off);
       const int cc = lane >> 4, ck = lane & 15;  // this lane stages copy cc, dword slot ck
       // global source of the 4 codes of columns 4D+cc..4D+cc+3 (an aligned dword of a shifted copy)
-      auto code_src = [&](int D) {
+      auto code_src = [&](int D) __attribute__((always_inline)) {
         const int g = 4 * D + cc - 1 + MSA_CPAD;
         return cod_pair + ((size_t)(g & (MSA_NCOPY - 1)) * a.cod_copy + (g & ~(MSA_NCOPY - 1))) / 4;
       };
-      auto code_put = [&](int D, unsigned v) {
+      auto code_put = [&](int D, unsigned v) __attribute__((always_inline)) {
         const int d = D & (MSA_CRING / 4 - 1);
         cring[cc * CRW + d] = v;
         if (d < 16) cring[cc * CRW + d + MSA_CRING / 4] = v;
       };
       // dword range of copy cc covering columns (a_, b_]
-      auto drange = [&](int a_, int b_, int& dlo, int& dhi) {
+      auto drange = [&](int a_, int b_, int& dlo, int& dhi) __attribute__((always_inline)) {
         dlo = ((a_ + 1 - cc - 3) >> 2);
         dhi = ((b_ - cc) >> 2);
       };
@@ -566,7 +567,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
         staged = hi1;
       }
       // issue the loads for columns needed at phase x into slot `sl`; commit later
-      auto code_issue = [&](int x, int sl) {
+      auto code_issue = [&](int x, int sl) __attribute__((always_inline)) {
         const int hi = need_hi(x);
         int dlo, dhi;
         drange(staged, hi, dlo, dhi);
@@ -580,7 +581,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
         if (cok[sl]) cval[sl] = *code_src(D);
         staged = max(staged, hi);
       };
-      auto code_commit = [&](int sl) {
+      auto code_commit = [&](int sl) __attribute__((always_inline)) {
         if (cok[sl]) code_put(cD[sl], cval[sl]);
       };
 
@@ -621,7 +622,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
       const bool border = (k0 == 0);  // the item holds the pair's first stripe: stage the DP's row 0
       // all staging / sinking works in 16-column chunks; phase p = chunks [CPP*p, CPP*p + CPP)
       const int nch0 = s0.P * CPP;
-      auto commit_border = [&](int c) {
+      auto commit_border = [&](int c) __attribute__((always_inline)) {
         const int v = lane >> 4, l = lane & 15;
         int bv[3];
         border_top<ALG>(kp, s0.cs + 16 * c + l, bv);
@@ -645,7 +646,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
       }
       const int* ring_last = rings + ((((sl_idx / W) & 1) * W + sl_idx % W) * NC) * MSA_RING;
       unsigned long long* g_out = a.gbuf + (size_t)group * NC * a.gbuf_stride;
-      auto sink_phase = [&](int q) {
+      auto sink_phase = [&](int q) __attribute__((always_inline)) {
         if (!sink || q < 0 || q >= sl.P) return;
         const int v = lane >> 4, l = lane & 15;
         if (v < NC) {
@@ -835,7 +836,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
       const int cj0 = sg.cs - lane;                // column of this lane at step 0
       const unsigned* cr_base = cring + (cj0 & 3) * CRW;
       const int cd0 = cj0 >> 2;                    // floor: absolute dword index at step 0
-      auto load_codes = [&](const int q) {
+      auto load_codes = [&](const int q) __attribute__((always_inline)) {
         if constexpr (LDSCODE) {
           const unsigned* cp = cr_base + ((cd0 + (KS / 4) * q) & (MSA_CRING / 4 - 1));
 #pragma unroll
@@ -889,9 +890,10 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
       unsigned long long* const g_out = a.gbuf + (size_t)group * NC * a.gbuf_stride;
       const size_t obase = (size_t)pd.out_off + (size_t)ks * pd.pmax * MSA_K * 64;  // pmax: 16-step blocks
 
-      auto run_phase = [&](const int q, auto MASKED_, auto INMASK_) {
+      auto run_phase = [&](const int q, auto MASKED_, auto INMASK_, auto FIN_) __attribute__((always_inline)) {
         constexpr bool MASKED = decltype(MASKED_)::value;  // per-lane start/end checks
         constexpr bool INMASK = decltype(INMASK_)::value;  // input columns beyond the producer's last
+        constexpr bool FIN = decltype(FIN_)::value;        // capture the state at each row's last column
         // ---- all LDS reads of the phase up front (one exposed latency per phase) ----
         int IN[NC][KS];
         {
@@ -917,11 +919,13 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
           }
 #endif
           if constexpr (INMASK) {
+            if (sg.cs + KS * q + KS - 1 > out_chi) {  // uniform: only the phases past the producer's end
 #pragma unroll
-            for (int k = 0; k < KS; ++k) {
-              const bool o = sg.cs + KS * q + k > out_chi;
+              for (int k = 0; k < KS; ++k) {
+                const bool o = sg.cs + KS * q + k > out_chi;
 #pragma unroll
-              for (int v = 0; v < NC; ++v) IN[v][k] = o ? MSA_NEG : IN[v][k];
+                for (int v = 0; v < NC; ++v) IN[v][k] = o ? MSA_NEG : IN[v][k];
+              }
             }
           }
         }
@@ -975,13 +979,26 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
             int cr[3];
             int ct = gdiag + kp.gap_open * t;
             if constexpr (ALG == MSA_ALG_SWL) asm("" : "+s"(ct));  // one SGPR feeds both the floor and H
-            const unsigned d = step<ALG, OUT, MASKED, TRACKPOS>(kp, L, inv, s, t, ct, cr, hv[k]);
+            const unsigned d = step<ALG, OUT, MASKED, TRACKPOS, FIN>(kp, L, inv, s, t, ct, cr, hv[k]);
 #pragma unroll
             for (int v = 0; v < NC; ++v) hist[v][k] = cr[v];
             if constexpr (SHREG) shreg = dpp_shl1(cr[0], shreg);
             dq |= d << (8 * kk);
           }
           dirw[u] = dq;
+          if constexpr (!SHREG) {
+            // lane 63 hands this quad's carried values to the next stripe right
+            // away (keeps only 4 steps of history live: no register spills at NC=3)
+            if (snk != SNK_NONE && lane == 63) {
+              const int x = (sg.cs + KS * q + 4 * u - 63 - out_cs + out_add) & out_mask;  // multiple of 4
+              if (x >= 0 && x <= out_lim) {
+#pragma unroll
+                for (int v = 0; v < NC; ++v)
+                  *reinterpret_cast<int4*>(out_ptr + x + v * out_vs) =
+                      make_int4(hist[v][4 * u], hist[v][4 * u + 1], hist[v][4 * u + 2], hist[v][4 * u + 3]);
+              }
+            }
+          }
           // cell outputs: one 1 KiB coalesced store per wave per 4 steps
           if constexpr (OUT == MSA_OUT_H) {
             int4 h4;
@@ -1024,21 +1041,6 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
               if (x >= 0 && xm < out_lim + 4) out_ptr[xm] = shreg;
             }
           }
-        } else if (snk != SNK_NONE && lane == 63) {
-          // (in 16-column chunks: the ring offset is only 16-aligned, each chunk wraps on its own)
-#pragma unroll
-          for (int h = 0; h < CPP; ++h) {
-            const int x = (sg.cs + KS * q + 16 * h - 63 - out_cs + out_add) & out_mask;  // multiple of 16
-            if (x >= 0 && x + 12 <= out_lim) {
-              int* dst = out_ptr + x;
-#pragma unroll
-              for (int v = 0; v < NC; ++v)
-#pragma unroll
-                for (int u = 4 * h; u < 4 * h + 4; ++u)
-                  *reinterpret_cast<int4*>(dst + v * out_vs + 4 * (u - 4 * h)) =
-                      make_int4(hist[v][4 * u], hist[v][4 * u + 1], hist[v][4 * u + 2], hist[v][4 * u + 3]);
-            }
-          }
         }
       };
       using T_ = std::true_type;
@@ -1050,23 +1052,28 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
       const int lim = min(sg.mask_hi, out_chi - sg.cs) - (KS - 1);
       const int qa = uni(min(P, sg.mask_lo <= 0 ? 0 : (sg.mask_lo + KS - 1) / KS));
       const int qb = uni(max(qa, min(P, lim >= 0 ? lim / KS + 1 : 0)));
-      auto run_range = [&](const int qb_, const int qe_, auto MASKED_, auto INMASK_) {
+      auto run_range = [&](const int qb_, const int qe_, auto MASKED_, auto INMASK_, auto FIN_) __attribute__((always_inline)) {
         for (int q = qb_; q < qe_; ++q) {
-          run_phase(q, MASKED_, INMASK_);
+          run_phase(q, MASKED_, INMASK_, FIN_);
           MSA_SYNC(ph + q);
         }
       };
+      const bool fin_stripe = uni(ks == S_pair - 1);
       if constexpr (SWK) {
         // no state masking; only the inputs past the producer's last column
         // (never written into the ring / granules) are replaced by -inf
         const int li = out_chi - sg.cs - (KS - 1);
         const int qi = uni(min(P, li >= 0 ? li / KS + 1 : 0));
-        run_range(0, qi, F_{}, F_{});
-        run_range(qi, P, F_{}, T_{});
+        run_range(0, qi, F_{}, F_{}, F_{});
+        run_range(qi, P, F_{}, T_{}, F_{});
+      } else if (fin_stripe) {
+        run_range(0, qa, T_{}, T_{}, T_{});
+        run_range(qa, qb, F_{}, F_{}, F_{});
+        run_range(qb, P, T_{}, T_{}, T_{});
       } else {
-        run_range(0, qa, T_{}, T_{});
-        run_range(qa, qb, F_{}, F_{});
-        run_range(qb, P, T_{}, T_{});
+        run_range(0, qa, T_{}, T_{}, F_{});
+        run_range(qa, qb, F_{}, F_{}, F_{});
+        run_range(qb, P, T_{}, T_{}, F_{});
       }
       ph += P;
       // ---- stripe finalize ----

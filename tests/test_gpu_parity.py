@@ -244,3 +244,39 @@ def test_reference_harness_linked_against_compat(tmp_path):
     kat = json.loads((GOLDEN / "kat.json").read_text())
     want = [h for h in kat["harness"] if (h["a"], h["b"], h["L"]) == (2, 15, 50)][0]
     assert hashlib.md5(block.encode()).hexdigest() == want["stdout_md5"], block
+
+
+@pytest.mark.parametrize("m,n", [(65, 70), (129, 129), (1, 5), (64, 1), (193, 200), (257, 64), (70, 65)])
+def test_reference_gotoh_ragged_edges(oracle, dev, m, n):
+    """Shapes whose last stripe has one row (m = 64k+1) or one column: stdout, tables, partitions vs the oracle."""
+    from cse305_parallel_sequence_alignment_amd import api
+
+    rng = np.random.default_rng(m * 1000 + n)
+    A, B = rs(rng, m), rs(rng, n)
+    t, sc = api.main_alignment_text(b"\0" + A, b"\0" + B, m, n, 8, 1, 2)
+    to, so = oracle.main_alignment_text(A, B, 1.0, 2.0)
+    assert (t, sc) == (to, so)
+    for st in (-1, -2, -3, 1, 2, 3):
+        sp = api.Subproblem(b"\0" + A, b"\0" + B, m, n, 0, 0, 1, st, -1, 1, 2)
+        sp.compute_tables()
+        T1, T2, T3, _ = oracle.subproblem_tables(A, B, st, 1.0, 2.0)
+        for x, y in zip((sp.T1, sp.T2, sp.T3), (T1, T2, T3)):
+            assert np.array_equal(x, y), (m, n, st)
+    if m >= 4 and n >= 4:
+        got = [a.as_tuple() for a in api.findPartialBalancedPartitionParallel(A, B, m, n, 4, 1, 2, 1, 1)]
+        assert got == oracle.partial_partition(A, B, 4, 1.0, 2.0, 1, 1)
+
+
+@pytest.mark.parametrize("m,n,w", [(65, 70, 8), (129, 130, 16), (193, 193, 64)])
+def test_nw_banded_single_row_stripe(oracle, dev, LB, m, n, w):
+    import torch
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+
+    rng = np.random.default_rng(m + 7 * w)
+    A, B = rs(rng, m), rs(rng, n)
+    pl = Plan(LB.NW_BANDED, LB.CELLS_H, [m], [n], [0], [0], match=1, mismatch=0, gap_open=3, gap_extend=1, band=w)
+    H = torch.empty(pl.cells_elems, dtype=torch.int32, device=dev)
+    pl.run(_dev(A, dev), _dev(B, dev), H)
+    score, Ho = oracle.banded_ref(A, B, w, 1.0, 2.0, want_h=True)
+    assert pl.results()[0]["score"] == int(score)
+    assert pl.checksum(H) == oracle.checksum_h(Ho, w)
