@@ -56,7 +56,7 @@ int ensure_device() {
 
 int nc_of(int alg) {
   switch (alg) {
-    case MSA_ALG_SWL: return 1;
+    case MSA_ALG_SWL: case MSA_ALG_SWL0: return 1;
     case MSA_ALG_SWA: case MSA_ALG_NWA: return 2;
     default: return 3;
   }
@@ -66,7 +66,7 @@ typedef void (*kfn_t)(KArgs);
 
 // single-pair phase length: 32 steps for one carried value (SW linear); 16 when
 // two or three values per cell are carried (register pressure: no spills)
-constexpr int ks_single(int alg) { return alg == MSA_ALG_SWL ? MSA_KS_SINGLE : 16; }
+constexpr int ks_single(int alg) { return (alg == MSA_ALG_SWL || alg == MSA_ALG_SWL0) ? MSA_KS_SINGLE : 16; }
 
 template <int ALG, int OUT, bool TP>
 kfn_t kf(bool sgl) {
@@ -81,6 +81,10 @@ kfn_t pick_kernel(int alg, int out, int tp, bool sgl) {
     case MSA_ALG_SWL:
       if (out == MSA_OUT_NONE) K3(MSA_ALG_SWL, MSA_OUT_NONE);
       if (out == MSA_OUT_H) K3(MSA_ALG_SWL, MSA_OUT_H);
+      break;
+    case MSA_ALG_SWL0:
+      if (out == MSA_OUT_NONE) K3(MSA_ALG_SWL0, MSA_OUT_NONE);
+      if (out == MSA_OUT_H) K3(MSA_ALG_SWL0, MSA_OUT_H);
       break;
     case MSA_ALG_SWA:
       if (out == MSA_OUT_NONE) K3(MSA_ALG_SWA, MSA_OUT_NONE);
@@ -199,14 +203,20 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   int out_mode = desc->cells;
   int kalg;
   switch (alg) {
-    case MSA_SW_LINEAR: kalg = MSA_ALG_SWL; break;
+    case MSA_SW_LINEAR:
+#ifdef MSA_NO_SWL0
+      kalg = MSA_ALG_SWL;
+#else
+      kalg = (desc->match >= 0 && desc->mismatch >= 0) ? MSA_ALG_SWL0 : MSA_ALG_SWL;
+#endif
+      break;
     case MSA_SW_AFFINE: kalg = MSA_ALG_SWA; break;
     case MSA_NW_BANDED: kalg = MSA_ALG_NWA; break;
     case MSA_REF_GOTOH: kalg = MSA_ALG_REF; break;
     case MSA_PARTIAL: kalg = MSA_ALG_PART; break;
     default: delete P; return MSA_ERR_ARG;
   }
-  const int tp = (kalg == MSA_ALG_SWL || kalg == MSA_ALG_SWA) ? (desc->track_end ? 1 : 0) : 0;
+  const int tp = (kalg == MSA_ALG_SWL || kalg == MSA_ALG_SWL0 || kalg == MSA_ALG_SWA) ? (desc->track_end ? 1 : 0) : 0;
   if (desc->single && desc->n_pairs != 1) { delete P; return MSA_ERR_ARG; }
   // A banded pair has only ~(2*band+64)/(64*lag) stripes in flight at once:
   // one workgroup cycling its waves over all stripes (the batch kernel, wrap
@@ -232,7 +242,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   kp.mismatch = desc->mismatch;
   kp.gap_open = desc->gap_open;
   kp.gap_ext = desc->gap_extend;
-  if (kalg == MSA_ALG_SWL) kp.gap_open = kp.gap_ext = desc->gap_extend;
+  if (kalg == MSA_ALG_SWL || kalg == MSA_ALG_SWL0) kp.gap_open = kp.gap_ext = desc->gap_extend;
   kp.h = desc->gap_open - desc->gap_extend;
   kp.start_type = desc->start_type;
   kp.band = band;
@@ -247,7 +257,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   for (int64_t p = 0; p < desc->n_pairs; ++p) {
     const int64_t m = desc->m[p], n = desc->n[p];
     if (m <= 0 || n <= 0 || m > (1 << 26) || n > (1 << 26)) { delete P; return MSA_ERR_ARG; }
-    if (kalg == MSA_ALG_SWL) {
+    if (kalg == MSA_ALG_SWL || kalg == MSA_ALG_SWL0) {
       // shifted recurrence G = H + g*(i+j): G must stay far from the -2^30 sentinel
       // and from int32 overflow; the profile byte holds score + 2g
       const int64_t g = kp.gap_open;
@@ -419,7 +429,7 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
   a.cod_copy = P->cod_copy;
   HIPCHK(hipMemsetAsync(P->d_ticket, 0, 64, st));
   {
-    const unsigned virt = (P->kp.alg == MSA_ALG_SWL || P->kp.alg == MSA_ALG_SWA) ? MSA_VIRT_CODE : 0u;
+    const unsigned virt = (P->kp.alg == MSA_ALG_SWL || P->kp.alg == MSA_ALG_SWL0 || P->kp.alg == MSA_ALG_SWA) ? MSA_VIRT_CODE : 0u;
     hipLaunchKernelGGL(stage_codes_kernel, dim3(64, (unsigned)P->segs.size()), dim3(256), 0, st, dB, P->d_segs,
                        (int)P->segs.size(), P->d_cod, (long long)P->cod_copy, virt);
     HIPCHK(hipGetLastError());
@@ -429,7 +439,7 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
   hipLaunchKernelGGL(P->fn, dim3(P->grid), dim3(waves * 64), P->lds_bytes, st, a);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(P->ev1, st));
-  const int sw = (P->kp.alg == MSA_ALG_SWL || P->kp.alg == MSA_ALG_SWA) ? 1 : 0;
+  const int sw = (P->kp.alg == MSA_ALG_SWL || P->kp.alg == MSA_ALG_SWL0 || P->kp.alg == MSA_ALG_SWA) ? 1 : 0;
   const int np = (int)P->d.n_pairs;
   hipLaunchKernelGGL(reduce_pairs_kernel, dim3((np + 255) / 256), dim3(256), 0, st, P->d_pairs, P->d_meta, np, sw,
                      P->d_res);

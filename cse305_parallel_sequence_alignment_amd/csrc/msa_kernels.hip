@@ -64,6 +64,9 @@ namespace msa {
 
 template <int ALG> struct Tr;
 template <> struct Tr<MSA_ALG_SWL> { static constexpr int NC = 1; };
+template <> struct Tr<MSA_ALG_SWL0> { static constexpr int NC = 1; };
+// SW linear in shifted space (either kernel id)
+constexpr bool swlin(int alg) { return alg == MSA_ALG_SWL || alg == MSA_ALG_SWL0; }
 template <> struct Tr<MSA_ALG_SWA> { static constexpr int NC = 2; };
 template <> struct Tr<MSA_ALG_NWA> { static constexpr int NC = 2; };
 template <> struct Tr<MSA_ALG_REF> { static constexpr int NC = 3; };
@@ -140,8 +143,9 @@ struct KArgs {
 template <int ALG>
 __device__ __forceinline__ void border_top(const msa_kparams& kp, int c, int (&v)[3]) {
   // Row 0 of the DP at column c (c may be < 0: unused, return NEG).
-  if constexpr (ALG == MSA_ALG_SWL) {
-    v[0] = c >= 0 ? kp.gap_open * c : MSA_NEG;  // G(0,c) = H(0,c) + g*c = g*c
+  if constexpr (swlin(ALG)) {
+    // G(0,c) = H(0,c) + g*c = g*c; SWL0 also on the virtual columns c < 0
+    v[0] = (c >= 0 || ALG == MSA_ALG_SWL0) ? kp.gap_open * c : MSA_NEG;
     v[1] = MSA_NEG;
     v[2] = MSA_NEG;
   } else if constexpr (ALG == MSA_ALG_SWA) {
@@ -179,7 +183,7 @@ __device__ __forceinline__ void border_top(const msa_kparams& kp, int c, int (&v
 template <int ALG>
 __device__ __forceinline__ void border_left(const msa_kparams& kp, int i, int (&v)[3]) {
   // Column 0 of row i (i >= 1), state order of each algorithm.
-  if constexpr (ALG == MSA_ALG_SWL) {
+  if constexpr (swlin(ALG)) {
     v[0] = kp.gap_open * i;  // G(i,0) = H(i,0) + g*i
     v[1] = MSA_NEG;
     v[2] = MSA_NEG;
@@ -239,6 +243,15 @@ __device__ __forceinline__ unsigned step(const msa_kparams& kp, LaneState<ALG>& 
     nS[0] = imax3(x, up, L.S[0]);
     // opaque: keeps G a real per-step value (otherwise LLVM flattens the
     // running max3 chain and distributes the "- ct" over every term)
+    asm("" : "+v"(nS[0]));
+    L.U[0] = up;
+  } else if constexpr (ALG == MSA_ALG_SWL0) {
+    // all scores >= 0: G(i-1,j-1) + s + 2g >= g*(i+j) whenever the diagonal
+    // cell satisfies its own floor, so (by induction from the borders) the
+    // zero floor never binds and is dropped.  Virtual columns score 0, which
+    // keeps G = g*(i+j) (H = 0) on every cell left of column 1.
+    const int up = dpp_shr1(in[0], L.S[0]);
+    nS[0] = imax3(L.U[0] + s, up, L.S[0]);
     asm("" : "+v"(nS[0]));
     L.U[0] = up;
   } else if constexpr (ALG == MSA_ALG_SWA) {
@@ -302,14 +315,14 @@ __device__ __forceinline__ unsigned step(const msa_kparams& kp, LaneState<ALG>& 
     L.U[1] = u1;
     L.U[2] = u2;
   }
-  constexpr int NS = (ALG == MSA_ALG_SWL) ? 1 : 3;
+  constexpr int NS = swlin(ALG) ? 1 : 3;
   if constexpr (MASKED) {
     const bool before = t < L.tmin;
     const bool after = t > L.tmax;
 #pragma unroll
     for (int v = 0; v < NS; ++v) nS[v] = before ? L.LB[v] : (after ? MSA_NEG : nS[v]);
-    if constexpr (ALG == MSA_ALG_SWL || ALG == MSA_ALG_SWA) {
-      const int hv = (ALG == MSA_ALG_SWL) ? nS[0] - ct : nS[0];
+    if constexpr (swlin(ALG) || ALG == MSA_ALG_SWA) {
+      const int hv = swlin(ALG) ? nS[0] - ct : nS[0];
       hout = hv;
       if (!before && !after) {
         if constexpr (TRACKPOS) {
@@ -325,8 +338,8 @@ __device__ __forceinline__ unsigned step(const msa_kparams& kp, LaneState<ALG>& 
       }
     }
   } else {
-    if constexpr (ALG == MSA_ALG_SWL || ALG == MSA_ALG_SWA) {
-      const int hv = (ALG == MSA_ALG_SWL) ? nS[0] - ct : nS[0];
+    if constexpr (swlin(ALG) || ALG == MSA_ALG_SWA) {
+      const int hv = swlin(ALG) ? nS[0] - ct : nS[0];
       hout = hv;
       if constexpr (TRACKPOS) {
         if (hv > L.best) { L.best = hv; L.bt = t; }
@@ -338,7 +351,7 @@ __device__ __forceinline__ unsigned step(const msa_kparams& kp, LaneState<ALG>& 
 #pragma unroll
   for (int v = 0; v < NS; ++v) L.S[v] = nS[v];
   // carried values (what the lane below / next stripe needs)
-  if constexpr (ALG == MSA_ALG_SWL) {
+  if constexpr (swlin(ALG)) {
     carry[0] = nS[0];
   } else if constexpr (ALG == MSA_ALG_SWA || ALG == MSA_ALG_NWA) {
     carry[0] = nS[0];
@@ -375,6 +388,11 @@ enum Snk { SNK_NONE = 0, SNK_RING = 1, SNK_ROW = 2, SNK_GLOBAL = 3 };
 // Phase barrier.  The diagnostic build (-DMSA_STAMPS) records s_memtime just
 // before and after every barrier of every wave: stamps[((item*16 + wave)*4096
 // + phase)*2 + {0,1}] (phases >= 4096 and items >= 64 are not recorded).
+#ifdef MSA_DBG_NO_SYNC
+#define MSA_BARRIER_() do {} while (0)  // timing experiments only: results are garbage
+#else
+#define MSA_BARRIER_() __syncthreads()
+#endif
 #ifdef MSA_STAMPS
 #ifdef MSA_STAMPS_RT
 #define MSA_CLOCK() __builtin_amdgcn_s_memrealtime()  // chip-wide 100 MHz: comparable across XCDs
@@ -387,7 +405,7 @@ enum Snk { SNK_NONE = 0, SNK_RING = 1, SNK_ROW = 2, SNK_GLOBAL = 3 };
     const bool rec__ = a.stamps && lane == 0 && ph__ < 4096 && item < 64;                   \
     const size_t o__ = (((size_t)item * 16 + w) * 4096 + ph__) * 4;                          \
     if (rec__) a.stamps[o__] = MSA_CLOCK();                                                 \
-    __syncthreads();                                                                        \
+    MSA_BARRIER_();                                                                         \
     if (rec__) a.stamps[o__ + 1] = MSA_CLOCK();                                             \
   } while (0)
 #define MSA_MARK(ph_, slot_)                                                                \
@@ -397,7 +415,7 @@ enum Snk { SNK_NONE = 0, SNK_RING = 1, SNK_ROW = 2, SNK_GLOBAL = 3 };
       a.stamps[(((size_t)item * 16 + w) * 4096 + ph__) * 4 + (slot_)] = MSA_CLOCK();          \
   } while (0)
 #else
-#define MSA_SYNC(ph_) __syncthreads()
+#define MSA_SYNC(ph_) MSA_BARRIER_()
 #define MSA_MARK(ph_, slot_) do {} while (0)
 #endif
 
@@ -442,7 +460,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
   // Smith-Waterman kernels never mask: columns outside [1, n] carry the
   // virtual code whose score (MSA_VIRT_SCORE) keeps every out-of-matrix cell
   // strictly below a real cell, so the plain recurrence runs over them.
-  constexpr bool SWK = (ALG == MSA_ALG_SWL || ALG == MSA_ALG_SWA);
+  constexpr bool SWK = (swlin(ALG) || ALG == MSA_ALG_SWA);
   constexpr int LA = (MSA_LOAD_AHEAD * 16 + KS - 1) / KS;  // loader prefetch depth in phases
   extern __shared__ __attribute__((aligned(16))) int smem[];
   const msa_kparams& kp = a.kp;
@@ -784,11 +802,15 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
       StripeGeom sg = sched[cur];
       sg.T = uni(sg.T); sg.P = uni(sg.P); sg.cs = uni(sg.cs); sg.lead = uni(sg.lead);
       sg.mask_lo = uni(sg.mask_lo); sg.mask_hi = uni(sg.mask_hi); sg.c_hi = uni(sg.c_hi);
+      // row code of this lane: a cold HBM load, issued before the idle phases
+      // (on the critical path of the wavefront if it waited for the stripe start)
+      const int ks = k0 + cur;  // pair-local stripe index
+      const int row_i = 64 * ks + lane + 1;
+      const unsigned ac = (row_i <= m) ? (a.A[pd.a_off + row_i - 1] & 7u) : 0u;
       for (; ph < sg.T; ++ph) MSA_SYNC(ph);
       // ---- stripe init ----
-      const int ks = k0 + cur;  // pair-local stripe index
       LaneState<ALG> L;
-      L.i = 64 * ks + lane + 1;
+      L.i = row_i;
       const int ivalid = min(L.i, m);
       L.tmin = jlo_of(L.i, kp.band) - sg.cs + lane;
       L.tmax = (L.i <= m) ? jhi_of(L.i, n, kp.band) - sg.cs + lane : -1;
@@ -804,21 +826,27 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
       const int gdiag = kp.gap_open * (64 * ks + 1 + sg.cs);  // SWL: g*(i+j) at step 0, same for all lanes
       // SWL: the lane starts left of the matrix on virtual cells with H = 0,
       // i.e. G = g*(i+j); its left neighbour at step 0 is G = gdiag - g
-      if constexpr (ALG == MSA_ALG_SWL) L.S[0] = gdiag - kp.gap_open;
+      if constexpr (swlin(ALG)) {
+        L.S[0] = gdiag - kp.gap_open;      // G(i, cs-r-1)
+        L.U[0] = gdiag - 2 * kp.gap_open;  // G(i-1, cs-r-1)
+      }
       // substitution profile of this row (codes 0..7)
       {
-        const unsigned ac = (L.i <= m) ? (a.A[pd.a_off + L.i - 1] & 7u) : 0u;
         int sm, sx;
         if constexpr (ALG == MSA_ALG_REF || ALG == MSA_ALG_NWA) { sm = 1; sx = 0; }
         else if constexpr (ALG == MSA_ALG_PART) { sm = 0; sx = 1; }
-        else if constexpr (ALG == MSA_ALG_SWL) { sm = kp.match + 2 * kp.gap_open; sx = kp.mismatch + 2 * kp.gap_open; }
+        else if constexpr (swlin(ALG)) { sm = kp.match + 2 * kp.gap_open; sx = kp.mismatch + 2 * kp.gap_open; }
         else { sm = kp.match; sx = kp.mismatch; }
         const unsigned bx = (unsigned)(sx & 0xff) * 0x01010101u;
         unsigned lo = bx, hi = bx;
         const unsigned bm = (unsigned)(sm & 0xff);
         if (ac < 4) lo = (lo & ~(0xffu << (8 * ac))) | (bm << (8 * ac));
         else hi = (hi & ~(0xffu << (8 * (ac - 4)))) | (bm << (8 * (ac - 4)));
-        if constexpr (SWK) hi = (hi & 0x00ffffffu) | ((unsigned)(MSA_VIRT_SCORE & 0xff) << 24);
+        // virtual columns: SWL0 scores them 0, so (floor-free) G = g*(i+j), i.e.
+        // H = 0, holds exactly on every cell left of column 1 -- the border
+        // column itself; right of column n they never beat a real cell
+        if constexpr (ALG == MSA_ALG_SWL0) hi = (hi & 0x00ffffffu) | ((unsigned)((2 * kp.gap_open) & 0xff) << 24);
+        else if constexpr (SWK) hi = (hi & 0x00ffffffu) | ((unsigned)(MSA_VIRT_SCORE & 0xff) << 24);
         L.plo = lo;
         L.phi = hi;
       }
@@ -978,7 +1006,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
             for (int v = 0; v < NC; ++v) inv[v] = IN[v][k];
             int cr[3];
             int ct = gdiag + kp.gap_open * t;
-            if constexpr (ALG == MSA_ALG_SWL) asm("" : "+s"(ct));  // one SGPR feeds both the floor and H
+            if constexpr (swlin(ALG)) asm("" : "+s"(ct));  // one SGPR feeds both the floor and H
             const unsigned d = step<ALG, OUT, MASKED, TRACKPOS, FIN>(kp, L, inv, s, t, ct, cr, hv[k]);
 #pragma unroll
             for (int v = 0; v < NC; ++v) hist[v][k] = cr[v];
@@ -1007,7 +1035,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
                              imax3(hist[0][4 * u + 1], hist[1][4 * u + 1], hist[2][4 * u + 1]),
                              imax3(hist[0][4 * u + 2], hist[1][4 * u + 2], hist[2][4 * u + 2]),
                              imax3(hist[0][4 * u + 3], hist[1][4 * u + 3], hist[2][4 * u + 3]));
-            } else if constexpr (ALG == MSA_ALG_SWL || ALG == MSA_ALG_SWA) {
+            } else if constexpr (swlin(ALG) || ALG == MSA_ALG_SWA) {
               h4 = make_int4(hv[4 * u], hv[4 * u + 1], hv[4 * u + 2], hv[4 * u + 3]);
             } else {
               h4 = make_int4(hist[0][4 * u], hist[0][4 * u + 1], hist[0][4 * u + 2], hist[0][4 * u + 3]);
@@ -1028,7 +1056,11 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
         MSA_MARK(ph + q, 2);
         // hand the bottom row to the next stripe: lane 63, once per phase
         if constexpr (SHREG) {
+#ifdef MSA_DBG_NO_RING
+          if (snk == SNK_GLOBAL && lane >= 64 - KS) {  // keep cross-workgroup publishes
+#else
           if (snk != SNK_NONE && lane >= 64 - KS) {
+#endif
             const int kk_ = lane - (64 - KS);
             if (snk == SNK_GLOBAL) {
               // last stripe of the item: publish straight to the next workgroup
@@ -1078,7 +1110,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
       ph += P;
       // ---- stripe finalize ----
       msa_stripe_meta* md = a.meta + pd.stripe0 + ks;
-      if constexpr (ALG == MSA_ALG_SWL || ALG == MSA_ALG_SWA) {
+      if constexpr (swlin(ALG) || ALG == MSA_ALG_SWA) {
         // first max in row-major order: max best, then min row
         int b = (L.i <= m) ? L.best : INT32_MIN;
         int bi = L.i;

@@ -14,6 +14,8 @@ enum msa_alg {
   MSA_ALG_NWA = 2,   // reference Gotoh, start type -1, h>=0, values only (banded, C3)
   MSA_ALG_REF = 3,   // reference Gotoh T1/T2/T3, any start type, exact -inf
   MSA_ALG_PART = 4,  // partial.cpp Gotoh with int32 wrap semantics
+  MSA_ALG_SWL0 = 5,  // Smith-Waterman, linear gap, every substitution score >= 0 (plan's
+                     // choice for MSA_SW_LINEAR when match, mismatch >= 0: no zero floor)
 };
 
 // Per-cell outputs.

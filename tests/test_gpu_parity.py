@@ -36,39 +36,48 @@ def LB():
     return _lib
 
 
+# (match, mismatch, gap): a negative mismatch runs the floored kernel; all
+# scores >= 0 run the floor-free one (MSA_ALG_SWL0, zero-score virtual cells)
+SW_SCORINGS = [(2, -1, 1), (1, 0, 1), (3, 1, 2), (1, 0, 3)]
+
+
+@pytest.mark.parametrize("scoring", SW_SCORINGS)
 @pytest.mark.parametrize("single", [True, False])
-def test_sw_linear_H_small(oracle, dev, LB, single):
+def test_sw_linear_H_small(oracle, dev, LB, single, scoring):
     import torch
     from cse305_parallel_sequence_alignment_amd.plan import Plan
 
+    ma, mi, g = scoring
     rng = np.random.default_rng(7)
     for (m, n) in [(1, 1), (5, 7), (64, 64), (65, 100), (130, 70), (200, 513), (511, 300), (700, 650), (520, 40)]:
         A, B = rs(rng, m), rs(rng, n)
-        pl = Plan(LB.SW_LINEAR, LB.CELLS_H, [m], [n], [0], [0], match=2, mismatch=-1, gap_open=1, gap_extend=1,
+        pl = Plan(LB.SW_LINEAR, LB.CELLS_H, [m], [n], [0], [0], match=ma, mismatch=mi, gap_open=g, gap_extend=g,
                   track_end=True, single=single)
         H = torch.empty(pl.cells_elems, dtype=torch.int32, device=dev)
         pl.run(_dev(A, dev), _dev(B, dev), H)
         res = pl.results()[0]
         Hd = pl.deskew(H.cpu().numpy(), 0, pl.stripe_meta())
-        o = oracle.sw(A, B, 2, -1, 1, 1, want_h=True)
+        o = oracle.sw(A, B, ma, mi, g, g, want_h=True)
         assert (res["score"], tuple(res["end"])) == (o["score"], tuple(o["end"])), (m, n)
         assert np.array_equal(Hd[1:, 1:], o["H"][1:, 1:]), (m, n)
         assert pl.checksum(H) == oracle.checksum_h(o["H"])
 
 
-def test_sw_linear_single_multi_group(oracle, dev, LB):
+@pytest.mark.parametrize("scoring", [(2, -1, 1), (1, 0, 1)])
+def test_sw_linear_single_multi_group(oracle, dev, LB, scoring):
     """Single-pair mode across several workgroups (cross-WG row handoff), repeated launches."""
     import torch
     from cse305_parallel_sequence_alignment_amd.plan import Plan
 
+    ma, mi, g = scoring
     rng = np.random.default_rng(11)
     for (m, n) in [(1500, 1200), (3000, 2500)]:
         A, B = rs(rng, m), rs(rng, n)
-        pl = Plan(LB.SW_LINEAR, LB.CELLS_H, [m], [n], [0], [0], match=2, mismatch=-1, gap_open=1, gap_extend=1,
+        pl = Plan(LB.SW_LINEAR, LB.CELLS_H, [m], [n], [0], [0], match=ma, mismatch=mi, gap_open=g, gap_extend=g,
                   track_end=True, single=True)
         H = torch.empty(pl.cells_elems, dtype=torch.int32, device=dev)
         dA, dB = _dev(A, dev), _dev(B, dev)
-        o = oracle.sw(A, B, 2, -1, 1, 1, want_h=True)
+        o = oracle.sw(A, B, ma, mi, g, g, want_h=True)
         for _ in range(3):
             pl.run(dA, dB, H)
             res = pl.results()[0]
@@ -76,23 +85,25 @@ def test_sw_linear_single_multi_group(oracle, dev, LB):
             assert pl.checksum(H) == oracle.checksum_h(o["H"])
 
 
-def test_sw_linear_batch_ragged(oracle, dev, LB):
+@pytest.mark.parametrize("scoring", [(2, -1, 1), (1, 0, 1)])
+def test_sw_linear_batch_ragged(oracle, dev, LB, scoring):
     import torch
     from cse305_parallel_sequence_alignment_amd.plan import Plan
 
+    ma, mi, g = scoring
     rng = np.random.default_rng(11)
     sizes = [(1100, 1000), (600, 4000), (1300, 960), (64, 3000), (2000, 1500), (33, 17), (1, 5), (129, 1)]
     As = [rs(rng, m) for m, n in sizes]
     Bs = [rs(rng, n) for m, n in sizes]
     ao = np.cumsum([0] + [m for m, n in sizes])[:-1]
     bo = np.cumsum([0] + [n for m, n in sizes])[:-1]
-    pl = Plan(LB.SW_LINEAR, LB.CELLS_H, [m for m, n in sizes], [n for m, n in sizes], ao, bo, match=2, mismatch=-1,
-              gap_open=1, gap_extend=1, track_end=True, single=False)
+    pl = Plan(LB.SW_LINEAR, LB.CELLS_H, [m for m, n in sizes], [n for m, n in sizes], ao, bo, match=ma, mismatch=mi,
+              gap_open=g, gap_extend=g, track_end=True, single=False)
     H = torch.empty(pl.cells_elems, dtype=torch.int32, device=dev)
     pl.run(_dev(b"".join(As), dev), _dev(b"".join(Bs), dev), H)
     res, meta, Hh = pl.results(), pl.stripe_meta(), H.cpu().numpy()
     for k, (m, n) in enumerate(sizes):
-        o = oracle.sw(As[k], Bs[k], 2, -1, 1, 1, want_h=True)
+        o = oracle.sw(As[k], Bs[k], ma, mi, g, g, want_h=True)
         assert res[k]["score"] == o["score"] and tuple(res[k]["end"]) == tuple(o["end"]), (m, n)
         assert np.array_equal(pl.deskew(Hh, k, meta)[1:, 1:], o["H"][1:, 1:]), (m, n)
 
