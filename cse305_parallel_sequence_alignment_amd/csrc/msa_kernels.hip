@@ -372,6 +372,16 @@ __device__ __forceinline__ void gstore(unsigned long long* p, unsigned long long
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Cell-output stores (H / T2 / T3 / direction planes) are written once and
+// never read back by the kernel: non-temporal stores stream them at ~64 B/clk
+// per CU, where plain (write-allocate) stores saturate at ~8 B/clk per CU --
+// below what four stripe waves produce (scratch/stbw.hip measurement).
+typedef int msa_v4i __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void ntstore(int4* p, int4 v) {
+  const msa_v4i x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<msa_v4i*>(p));
+}
+
 enum Src { SRC_BORDER = 0, SRC_RING = 1, SRC_ROW = 2, SRC_GLOBAL = 3 };
 enum Snk { SNK_NONE = 0, SNK_RING = 1, SNK_ROW = 2, SNK_GLOBAL = 3 };
 
@@ -926,11 +936,6 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
         int IN[NC][KS];
         {
           const int* base = in_ptr + ((KS * q) & in_mask);
-#ifdef MSA_IN_LANE0
-          // only lane 0 consumes the row above (DPP old operand): read it with
-          // one active lane so the LDS returns 16 B instead of 1 KiB per read
-          if (lane == 0) {
-#endif
 #pragma unroll
           for (int v = 0; v < NC; ++v) {
 #pragma unroll
@@ -943,9 +948,6 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
               IN[v][4 * u + 0] = x.x; IN[v][4 * u + 1] = x.y; IN[v][4 * u + 2] = x.z; IN[v][4 * u + 3] = x.w;
             }
           }
-#ifdef MSA_IN_LANE0
-          }
-#endif
           if constexpr (INMASK) {
             if (sg.cs + KS * q + KS - 1 > out_chi) {  // uniform: only the phases past the producer's end
 #pragma unroll
@@ -970,7 +972,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
 #ifdef MSA_STAMPS
         {
           int z = IN[0][0] ^ (int)cw[0];
-          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           asm volatile("" ::"v"(z));
           MSA_MARK(ph + q, 3);
         }
@@ -1040,18 +1042,18 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
             } else {
               h4 = make_int4(hist[0][4 * u], hist[0][4 * u + 1], hist[0][4 * u + 2], hist[0][4 * u + 3]);
             }
-            hrow[u * 64] = h4;
+            ntstore(hrow + u * 64, h4);
           } else if constexpr (OUT == MSA_OUT_TAB) {
-            hrow[u * 64] = make_int4(hist[0][4 * u], hist[0][4 * u + 1], hist[0][4 * u + 2], hist[0][4 * u + 3]);
-            t2row[u * 64] = make_int4(hist[1][4 * u], hist[1][4 * u + 1], hist[1][4 * u + 2], hist[1][4 * u + 3]);
-            t3row[u * 64] = make_int4(hist[2][4 * u], hist[2][4 * u + 1], hist[2][4 * u + 2], hist[2][4 * u + 3]);
+            ntstore(hrow + u * 64, make_int4(hist[0][4 * u], hist[0][4 * u + 1], hist[0][4 * u + 2], hist[0][4 * u + 3]));
+            ntstore(t2row + u * 64, make_int4(hist[1][4 * u], hist[1][4 * u + 1], hist[1][4 * u + 2], hist[1][4 * u + 3]));
+            ntstore(t3row + u * 64, make_int4(hist[2][4 * u], hist[2][4 * u + 1], hist[2][4 * u + 2], hist[2][4 * u + 3]));
           }
         }
         if constexpr (OUT == MSA_OUT_DIR) {
 #pragma unroll
           for (int h = 0; h < CPP; ++h)
-            reinterpret_cast<uint4*>(a.outDir + obase)[(size_t)(CPP * q + h) * 64 + lane] =
-                make_uint4(dirw[4 * h], dirw[4 * h + 1], dirw[4 * h + 2], dirw[4 * h + 3]);
+            ntstore(reinterpret_cast<int4*>(a.outDir + obase) + (size_t)(CPP * q + h) * 64 + lane,
+                    make_int4((int)dirw[4 * h], (int)dirw[4 * h + 1], (int)dirw[4 * h + 2], (int)dirw[4 * h + 3]));
         }
         MSA_MARK(ph + q, 2);
         // hand the bottom row to the next stripe: lane 63, once per phase
