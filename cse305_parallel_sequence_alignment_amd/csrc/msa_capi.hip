@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <mutex>
 #include <new>
 #include <string>
@@ -17,6 +18,7 @@
 
 #include "../../include/msa.h"
 #include "msa_kernels.hip"
+#include "msa_flow.hip"
 
 using namespace msa;
 
@@ -109,6 +111,24 @@ kfn_t pick_kernel(int alg, int out, int tp, bool sgl) {
   return nullptr;
 }
 
+// single-pair SW linear (msa_flow.hip): pass 1 (chain), pass 2 (fill + H)
+kfn_t pick_flow(int alg, bool best, bool save) {
+  const bool fl = (alg == MSA_ALG_SWL);
+  if (best) return fl ? flow_kernel<true, true, false> : flow_kernel<false, true, false>;
+  if (save) return fl ? flow_kernel<true, false, true> : flow_kernel<false, false, true>;
+  return nullptr;
+}
+kfn_t pick_fill(int alg, int tp) {
+  const bool fl = (alg == MSA_ALG_SWL);
+  if (fl) return tp ? fill_kernel<true, true> : fill_kernel<true, false>;
+  return tp ? fill_kernel<false, true> : fill_kernel<false, false>;
+}
+
+int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return (v && *v) ? std::atoi(v) : dflt;
+}
+
 }  // namespace
 
 struct msa_plan {
@@ -122,6 +142,15 @@ struct msa_plan {
   int64_t cells_elems = 0;
   size_t lds_bytes = 0;
   int grid = 1;
+  int threads = 64;
+  bool flow = false;   // flow_kernel (single-pair SW linear) instead of stripe_kernel
+  bool flow2 = false;  // + fill_kernel pass (O_H)
+  kfn_t fn2 = nullptr;
+  int grid2 = 0;
+  int32_t* d_br = nullptr;
+  int32_t* d_snap = nullptr;
+  int4* d_blk = nullptr;
+  int brw = 0, nseg = 0, nblk = 0;
   int gbuf_stride = 0;
   kfn_t fn = nullptr;
   // device
@@ -226,11 +255,21 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   if (single && kalg == MSA_ALG_NWA && desc->band >= 0 && (int64_t)desc->band * 2 + 64 < desc->n[0] / 4) single = false;
 #endif
   P->d.single = single ? 1 : 0;
-  const int W = single ? MSA_WAVES_SINGLE : MSA_WAVES_BATCH;
+  // flow kernel: one SW-linear pair whose 8 LDS code copies fit next to the rings
+  // two-pass flow kernels: one SW-linear pair whose 8 LDS code copies fit next to the rings
+  const size_t flow_lds = (size_t)(FL_FLAGS + (FL_W + 1) * 256) * 4 + (size_t)FL_NCOPY * fl_code_bytes((int)desc->n[0]);
+  const bool flow = single && (kalg == MSA_ALG_SWL || kalg == MSA_ALG_SWL0) &&
+                    (out_mode == MSA_OUT_H || (out_mode == MSA_OUT_NONE && !tp)) &&
+                    env_int("MSA_FLOW", 1) != 0 && desc->m[0] > 0 && flow_lds <= 160 * 1024;
+  P->flow = flow;
+  P->flow2 = flow && out_mode == MSA_OUT_H;
+  const int W = flow ? FL_W : (single ? MSA_WAVES_SINGLE : MSA_WAVES_BATCH);
   P->W = W;
-  const int KS = single ? ks_single(kalg) : MSA_KS_BATCH;
+  const int KS = flow ? 16 : (single ? ks_single(kalg) : MSA_KS_BATCH);
   P->KS = KS;
-  P->fn = pick_kernel(kalg, out_mode, tp, single);
+  P->threads = (flow ? W + 2 : W + 1 + (single ? 1 : 0)) * 64;
+  P->fn = flow ? pick_flow(kalg, out_mode == MSA_OUT_NONE, out_mode == MSA_OUT_H) : pick_kernel(kalg, out_mode, tp, single);
+  if (P->flow2) P->fn2 = pick_fill(kalg, tp);
   if (!P->fn) { delete P; return MSA_ERR_UNSUPPORTED; }
   P->nc = nc_of(kalg);
   const int band = (kalg == MSA_ALG_NWA) ? desc->band : -1;
@@ -320,6 +359,10 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
                           (size_t)P->nc * kp.lds_row_words +
                           (single ? (size_t)4 * (MSA_CRING / 4 + 16) : 0);  // code ring
   P->lds_bytes = lds_ints * 4;
+  if (flow) {
+    kp.lds_code_bytes = fl_code_bytes((int)desc->n[0]);
+    P->lds_bytes = flow_lds;
+  }
   if (P->lds_bytes > 160 * 1024) {
     std::fprintf(stderr, "msa: problem needs %zu B of LDS per workgroup (> 160 KiB)\n", P->lds_bytes);
     delete P;
@@ -331,8 +374,8 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     return MSA_ERR_HIP;
   }
   int occ = 1;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)P->fn, (W + 1 + (single ? 1 : 0)) * 64,
-                                                   P->lds_bytes) != hipSuccess || occ < 1)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)P->fn, P->threads, P->lds_bytes) !=
+          hipSuccess || occ < 1)
     occ = 1;
   hipDeviceProp_t prop;
   int dev = 0;
@@ -340,6 +383,16 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   (void)hipGetDeviceProperties(&prop, dev);
   const int cap = prop.multiProcessorCount * std::min(occ, 2);
   P->grid = std::max(1, std::min(kp.n_items, cap));
+  if (flow) {
+    // items in 8 contiguous chunks, one per XCD (workgroup b takes tickets of chunk b % 8,
+    // round-robin placement puts it on XCD b % 8): consecutive items hand off inside one
+    // L2 except at 7 chunk seams.  Speed only: an item only waits on an earlier one and
+    // every workgroup is resident (one per CU, grid <= CUs), whatever the placement.
+    const int per_xcd = std::max(1, prop.multiProcessorCount / 8);
+    const int chunk = (kp.n_items + 7) / 8;
+    kp.sched_cap = chunk;
+    P->grid = 8 * std::max(1, std::min(chunk, per_xcd));
+  }
   // device buffers
   auto fail = [&](void) { msa_plan_destroy(P); return MSA_ERR_HIP; };
   if (hipMalloc(&P->d_pairs, sizeof(msa_pair_desc) * P->pairs.size()) != hipSuccess) return fail();
@@ -364,6 +417,16 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     if (hipMalloc(&P->d_gbuf, gb) != hipSuccess) return fail();
     if (hipMemset(P->d_gbuf, 0, gb) != hipSuccess) return fail();
   }
+  if (P->flow2) {
+    const int S = (int)((desc->m[0] + 63) / 64);
+    P->brw = 16 * P->pairs[0].pmax + 16;
+    P->nseg = (P->pairs[0].pmax + FL_PS - 1) / FL_PS;
+    P->nblk = S * P->nseg;
+    P->grid2 = (P->nblk + 3) / 4;
+    if (hipMalloc(&P->d_br, sizeof(int32_t) * (size_t)S * P->brw) != hipSuccess) return fail();
+    if (hipMalloc(&P->d_snap, sizeof(int32_t) * (size_t)P->nblk * 128) != hipSuccess) return fail();
+    if (hipMalloc(&P->d_blk, sizeof(int4) * (size_t)P->grid2 * 4) != hipSuccess) return fail();
+  }
   if (hipEventCreate(&P->ev0) != hipSuccess || hipEventCreate(&P->ev1) != hipSuccess) return fail();
   *out = P;
   return MSA_OK;
@@ -379,6 +442,9 @@ void msa_plan_destroy(msa_plan* P) {
   if (P->d_segs) (void)hipFree(P->d_segs);
   if (P->d_res) (void)hipFree(P->d_res);
   if (P->d_sum) (void)hipFree(P->d_sum);
+  if (P->d_br) (void)hipFree(P->d_br);
+  if (P->d_snap) (void)hipFree(P->d_snap);
+  if (P->d_blk) (void)hipFree(P->d_blk);
   if (P->ev0) (void)hipEventDestroy(P->ev0);
   if (P->ev1) (void)hipEventDestroy(P->ev1);
   delete P;
@@ -427,6 +493,11 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
   a.stamps = P->stamps;
   a.cod = P->d_cod;
   a.cod_copy = P->cod_copy;
+  a.br = P->d_br;
+  a.snap = P->d_snap;
+  a.blk = P->d_blk;
+  a.brw = P->brw;
+  a.nseg = P->nseg;
   HIPCHK(hipMemsetAsync(P->d_ticket, 0, 64, st));
   {
     const unsigned virt = (P->kp.alg == MSA_ALG_SWL || P->kp.alg == MSA_ALG_SWL0 || P->kp.alg == MSA_ALG_SWA) ? MSA_VIRT_CODE : 0u;
@@ -435,13 +506,21 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipEventRecord(P->ev0, st));
-  const int waves = P->W + 1 + (P->d.single ? 1 : 0);  // compute + loader (+ code wave, single pair)
-  hipLaunchKernelGGL(P->fn, dim3(P->grid), dim3(waves * 64), P->lds_bytes, st, a);
+  hipLaunchKernelGGL(P->fn, dim3(P->grid), dim3(P->threads), P->lds_bytes, st, a);
   HIPCHK(hipGetLastError());
+  if (P->flow2) {
+    hipLaunchKernelGGL(P->fn2, dim3(P->grid2), dim3(256), 0, st, a);
+    HIPCHK(hipGetLastError());
+  }
   HIPCHK(hipEventRecord(P->ev1, st));
+  if (P->flow2) {
+    hipLaunchKernelGGL(reduce_blocks_kernel, dim3(1), dim3(256), 0, st, (const int4*)P->d_blk, P->nblk, P->d_res);
+    HIPCHK(hipGetLastError());
+    return MSA_OK;
+  }
   const int sw = (P->kp.alg == MSA_ALG_SWL || P->kp.alg == MSA_ALG_SWL0 || P->kp.alg == MSA_ALG_SWA) ? 1 : 0;
   const int np = (int)P->d.n_pairs;
-  hipLaunchKernelGGL(reduce_pairs_kernel, dim3((np + 255) / 256), dim3(256), 0, st, P->d_pairs, P->d_meta, np, sw,
+  hipLaunchKernelGGL(reduce_pairs_kernel, dim3(np), dim3(64), 0, st, P->d_pairs, P->d_meta, np, sw,
                      P->d_res);
   HIPCHK(hipGetLastError());
   return MSA_OK;

@@ -1,0 +1,672 @@
+// msa_flow.hip -- single-pair Smith-Waterman (linear gap) in two passes: the
+// latency-bound DP chain, then a chip-wide recompute that writes H (config C2:
+// one 10k x 10k pair on one GPU).  Replaces, for this configuration, the
+// reference's row sweep Subproblem::compute_tables (subproblem_alignment.cpp:
+// 329-332; per-row T1/T3 :229-235, the omega prefix-max scan :237-249, :13-103).
+//
+// Pass 1 (flow_kernel) runs stripe_kernel's geometry (64-row stripes, lane r =
+// row 64s+r+1 at column cs+t-r in step t) as a flag-synchronised pipeline cut
+// down to the loop-carried chain.  Per DP step a compute wave issues one DPP
+// wave_shr:1 (the cell above, from lane r-1; lane 0 takes the producer's value
+// through the DPP `old` operand), one SDWA byte add (diagonal + score from a
+// v_perm'd profile word) and one v_max3:
+//     G(i,j) = max3(G(i-1,j-1) + s + 2g, G(i-1,j), G(i,j-1)),   G = H + g(i+j)
+// (X-space, X = H - g with a zero floor, when scores can be negative).  The
+// step time is the DPP -> v_max3 latency (~21 cycles measured on one wave);
+// nothing else sits on the chain:
+//   * waves 0..W-1 compute (one per SIMD), wave W io-in, wave W+1 io-out;
+//   * no s_barrier: a producer's lane 63 writes each 16-column block of its
+//     bottom row to an LDS ring and then bumps its phase counter; the consumer
+//     reads the counter, then the block (LDS executes one wave's DS
+//     instructions in issue order), half a phase ahead of use.  A slot is
+//     re-used once the consumer and io-out have passed it;
+//   * io-in: column codes into LDS (8 byte-shifted copies, one ds_read2_b64
+//     per lane per phase) ahead of the blocks it publishes, and the row above
+//     the workgroup (the previous workgroup's {epoch, value} granules, or row 0);
+//   * io-out: every link's blocks -> the bottom-row array BR (pass 2's input),
+//     the last link's also -> {epoch, value} granules for the next workgroup;
+//   * every FL_PS phases each lane's state (left, diagonal) -> SNAP;
+//   * items (W stripes) come from 8 per-XCD ticket chunks: consecutive items
+//     share an L2, and an item only ever waits on an earlier one.
+// Pass 2 (fill_kernel): every (stripe, FL_PS-phase segment) block restarts
+// from SNAP and BR, recomputes its cells with the same instructions, writes
+// int32 H in the skewed stripe layout (coalesced non-temporal 1 KiB stores)
+// and reduces its best cell.  Thousands of independent blocks fill the chip,
+// so H streams at HBM rate instead of stalling the chain (a 1 KiB store
+// stalls its wave ~40 cycles, longer than a DP step).
+#pragma once
+
+namespace msa {
+
+#ifndef FL_W
+#define FL_W 4          // compute waves per workgroup: one per SIMD
+#endif
+#define FL_RINGB 16     // ring blocks of 16 columns per link (256 columns)
+#define FL_OFF 95       // LDS code copy x, byte y <-> column y + x - FL_OFF (== CPAD-1 mod 16)
+#define FL_NCOPY 8      // byte-shifted LDS code copies (8-byte aligned 8-code reads)
+#define FL_FLAGS 128    // ints of flags at the start of LDS
+#define FL_PS 32        // phases per pass-2 segment (pass 1 saves its state every FL_PS phases)
+#define FL_SPIN_MAX (1u << 26)
+
+__host__ __device__ __forceinline__ int fl_cs(int k) { return -((16 - (k & 15)) & 15); }  // -((-k) mod 16)
+__host__ __device__ __forceinline__ int fl_P(int k, int m, int n) {
+  const int rlast = (m - 64 * k - 1 < 63) ? (m - 64 * k - 1) : 63;
+  return (n - fl_cs(k) + rlast) / 16 + 1;
+}
+// link k-1 -> k: ring block b holds columns cs_k + 16b .. +15 of row 64k;
+// producer phase q writes block q - fl_dq(k); its last block is fl_bmax(k)
+__host__ __device__ __forceinline__ int fl_delta(int kc) { return fl_cs(kc - 1) + 1 - fl_cs(kc); }
+__host__ __device__ __forceinline__ int fl_dq(int kc) { return 4 - fl_delta(kc) / 16; }
+__host__ __device__ __forceinline__ int fl_bmax(int kc, int m, int n) { return fl_P(kc - 1, m, n) - 1 - fl_dq(kc); }
+// bytes per LDS code copy for n columns (covers the prefetch one phase past a stripe's last)
+__host__ __device__ __forceinline__ int fl_code_bytes(int n) { return ((n + 208) + 15) & ~15; }
+
+// LDS accesses through explicit address-space-3 pointers: a generic pointer
+// would become a FLAT access (counted in vmcnt AND lgkmcnt, forcing full waits)
+typedef __attribute__((address_space(3))) int lds_int;
+typedef int fl_v4i __attribute__((ext_vector_type(4)));
+typedef unsigned fl_v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) fl_v4i lds_int4;
+__device__ __forceinline__ lds_int* L(int* p) { return (lds_int*)(p); }
+__device__ __forceinline__ int lds_vload(const int* p) { return *(volatile lds_int*)(p); }
+__device__ __forceinline__ void lds_vstore(int* p, int v) { *(volatile lds_int*)(p) = v; }
+#define FL_CBAR() asm volatile("" ::: "memory")
+// Diagnostic build (-DMSA_STAMPS): stamps[((item*16 + w)*4096 + q)*4 + slot]
+//   slot 0: s_memtime at phase start, 1: after its input wait, 2: s_memrealtime at phase start
+#ifdef MSA_STAMPS
+#define FL_STAMP(q_, slot_, v_)                                                                        \
+  do {                                                                                              \
+    if (a.stamps && lane == 0 && (q_) < 4096 && item < 64)                                           \
+      a.stamps[(((size_t)item * 16 + w) * 4096 + (q_)) * 4 + (slot_)] = (v_);                        \
+  } while (0)
+#else
+#define FL_STAMP(q_, slot_, v_) do {} while (0)
+#endif
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)(p);
+}
+// Inline-asm DS ops: the compiler does not count them, so every wait below is
+// explicit (s_waitcnt lgkmcnt(N), N = DS ops issued after the awaited one), and
+// every output stays live (named "+v" by its wait) until it has landed.
+__device__ __forceinline__ int ds_read_b32(unsigned a) {
+  int v;
+  asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+template <int OFF>
+__device__ __forceinline__ fl_v4i ds_read_b128(unsigned a) {
+  fl_v4i v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF) : "memory");
+  return v;
+}
+__device__ __forceinline__ fl_v4u ds_read2_b64(unsigned a) {
+  fl_v4u v;
+  asm volatile("ds_read2_b64 %0, %1 offset1:1" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+// slow path: re-read a block into the same registers (tied operands: no copies on the fast path)
+__device__ __forceinline__ void ds_reread_b128x4(unsigned a, fl_v4i (&in)[4]) {
+  asm volatile(
+      "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:16\n\t"
+      "ds_read_b128 %2, %4 offset:32\n\tds_read_b128 %3, %4 offset:48\n\ts_waitcnt lgkmcnt(0)"
+      : "+v"(in[0]), "+v"(in[1]), "+v"(in[2]), "+v"(in[3])
+      : "v"(a)
+      : "memory");
+}
+template <int N = 0>
+__device__ __forceinline__ void lgkm_wait(int& v) { asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(v) : "i"(N) : "memory"); }
+template <int N = 0>
+__device__ __forceinline__ void lgkm_wait_v(fl_v4i (&in)[4], fl_v4u& cw) {
+  asm volatile("s_waitcnt lgkmcnt(%5)" : "+v"(in[0]), "+v"(in[1]), "+v"(in[2]), "+v"(in[3]), "+v"(cw) : "i"(N) : "memory");
+}
+// Lane 63 alone: its 16 bottom-row values -> ring block, then the phase
+// counter (DS ops of one wave execute in order: the block lands first).
+// s_nop 4: an SALU exec write needs 5 wait states before a DPP op.
+__device__ __forceinline__ void ds_handoff(unsigned long long m63, unsigned ra, fl_v4i x0, fl_v4i x1, fl_v4i x2,
+                                           fl_v4i x3, unsigned pa, int pv) {
+  unsigned long long sv;
+  asm volatile(
+      "s_mov_b64 %[sv], exec\n\t"
+      "s_mov_b64 exec, %[m]\n\t"
+      "ds_write_b128 %[ra], %[x0]\n\t"
+      "ds_write_b128 %[ra], %[x1] offset:16\n\t"
+      "ds_write_b128 %[ra], %[x2] offset:32\n\t"
+      "ds_write_b128 %[ra], %[x3] offset:48\n\t"
+      "ds_write_b32 %[pa], %[pv]\n\t"
+      "s_mov_b64 exec, %[sv]\n\t"
+      "s_nop 4"
+      : [sv] "=&s"(sv)
+      : [m] "s"(m63), [ra] "v"(ra), [x0] "v"(x0), [x1] "v"(x1), [x2] "v"(x2), [x3] "v"(x3), [pa] "v"(pa),
+        [pv] "v"(pv)
+      : "memory");
+}
+
+// Substitution profile of a row: score + g (X-space) or + 2g (G-space) for
+// codes 0..7; code 7 = virtual column (outside [1, n]): score 0 without the
+// floor (keeps H = 0 left of column 1, never above a real cell right of n),
+// -100 with it.
+template <bool GS, bool FLOOR>
+__device__ __forceinline__ void fl_profile(int match, int mismatch, int g, unsigned ac, unsigned& plo, unsigned& phi) {
+  const int sh = GS ? 2 * g : g;
+  const int sm = match + sh, sx = mismatch + sh;
+  const unsigned bx = (unsigned)(sx & 0xff) * 0x01010101u;
+  unsigned lo = bx, hi = bx;
+  const unsigned bm = (unsigned)(sm & 0xff);
+  if (ac < 4) lo = (lo & ~(0xffu << (8 * ac))) | (bm << (8 * ac));
+  else hi = (hi & ~(0xffu << (8 * (ac - 4)))) | (bm << (8 * (ac - 4)));
+  const int sv = (FLOOR ? MSA_VIRT_SCORE : 0) + sh;
+  hi = (hi & 0x00ffffffu) | ((unsigned)(sv & 0xff) << 24);
+  plo = lo;
+  phi = hi;
+}
+
+// One DP step of every lane; returns the cell's G (G-space) or H (X-space).
+template <bool GS, bool FLOOR>
+__device__ __forceinline__ int fl_step(int in, int s, int& X, int& U, int g) {
+  const int up = dpp_shr1(in, X);
+  int h = imax3(U + s, up, X);
+  if constexpr (FLOOR) h = imax(h, 0);
+  asm("" : "+v"(h));  // keeps the chain a real per-step value
+  U = up;
+  X = GS ? h : h - g;
+  return h;
+}
+
+// FLOOR: scores may be negative (zero floor, X-space); otherwise G-space.
+// BEST: track the best cell in pass 1 (score-only plans: no pass 2).
+// SAVE: write BR and SNAP for pass 2.
+template <bool FLOOR, bool BEST, bool SAVE>
+__global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
+  constexpr bool GS = !FLOOR;
+  extern __shared__ __attribute__((aligned(16))) int smem[];
+  const msa_kparams& kp = a.kp;
+  const int lane = threadIdx.x & 63;
+  const int w = uni(threadIdx.x >> 6);
+  constexpr int W = FL_W;
+  // flags: [0] item; prog[l] 32+l (l = 0: io-in's published blocks, l = c+1:
+  // compute wave c's finished phases); rcons[l] 64+l (io-out: blocks of link l
+  // taken); dummy sink 96..127
+  int* flags = smem;
+  int* rings = smem + FL_FLAGS;                                          // [W+1 links][256]
+  uint8_t* codes = reinterpret_cast<uint8_t*>(rings + (W + 1) * 256);  // [8][L8]
+  const int L8 = kp.lds_code_bytes;
+  const msa_pair_desc pd = a.pairs[0];
+  const int m = pd.m, n = pd.n;
+  const int S = (m + 63) / 64;
+  const int g = kp.gap_ext;
+  const unsigned ep = kp.epoch;
+  const int grp = (int)(blockIdx.x & 7), chunk = kp.sched_cap;
+
+  for (;;) {
+    if (threadIdx.x == 0) {
+      const int t = atomicAdd(a.ticket + 4 + grp, 1);
+      flags[0] = (t < chunk) ? min(grp * chunk + t, kp.n_items) : kp.n_items;
+    }
+    if (threadIdx.x >= 16 && threadIdx.x < 128) flags[threadIdx.x] = 0;
+    __syncthreads();
+    const int item = uni(flags[0]);
+    if (item >= kp.n_items) break;
+    const int k0 = item * W;
+
+    if (w == W) {
+      // =================== io-in: codes + the row above stripe k0 ===================
+      int* ring = rings;
+      int* pub = flags + 32;
+      const int* cons = flags + 33;  // compute wave 0's finished phases = blocks it no longer needs
+      const int cs_c = fl_cs(k0);
+      const int Pc = fl_P(k0, m, n);
+      const int Bmax = (k0 == 0) ? Pc - 1 : min(Pc - 1, fl_bmax(k0, m, n));
+      const uint8_t* gcod = a.cod + pd.cod_off;
+      int Yr = 0;  // bytes [0, Yr) of every LDS code copy are loaded
+      auto load_codes = [&](int Y1) __attribute__((always_inline)) {
+        Y1 = min(Y1, L8);
+        const int tot = FL_NCOPY * ((Y1 - Yr) / 16);  // 16-byte chunks over all copies
+        for (int c0 = 0; c0 < tot; c0 += 4 * 64) {     // 4 loads in flight per lane
+          int4 v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int c = min(c0 + r * 64 + lane, tot - 1);
+            const int x = c & (FL_NCOPY - 1), y = Yr + 16 * (c >> 3);
+            v[r] = *reinterpret_cast<const int4*>(gcod + (size_t)x * a.cod_copy + (y + MSA_CPAD - 1 - FL_OFF));
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int c = c0 + r * 64 + lane;
+            const int x = c & (FL_NCOPY - 1), y = Yr + 16 * (c >> 3);
+            if (c < tot) *(lds_int4*)(codes + x * L8 + y) = fl_v4i{v[r].x, v[r].y, v[r].z, v[r].w};
+          }
+        }
+        Yr = max(Yr, Y1);
+      };
+      load_codes(1024);
+      const unsigned long long* g_in = a.gbuf + (size_t)(item > 0 ? item - 1 : 0) * a.gbuf_stride;
+      int b = 0;
+      int consv = 0;
+      unsigned spins = 0;
+      while (b <= Bmax) {
+        if (Yr < L8 && Yr < 16 * b + 768) load_codes(Yr + 1024);
+        // up to 16 blocks (256 columns) per round trip: lane l, load r -> block b + 4r + l/16
+        int val[4];
+        int nb = 0;
+        if (k0 == 0) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int col = cs_c + 16 * b + 64 * r + lane;
+            val[r] = GS ? g * col : -g;  // row 0: H = 0
+          }
+          nb = min(16, Bmax - b + 1);
+        } else {
+          unsigned long long gv[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int col = cs_c + 16 * b + 64 * r + lane;
+            const int ci = min(max(col + MSA_GOFF, 0), a.gbuf_stride - 1);
+            gv[r] = gload(g_in + ci);
+          }
+          bool run = true;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            val[r] = (int)(unsigned)gv[r];
+            const int blk = b + 4 * r + (lane >> 4);
+            const bool ok = (blk > Bmax) || ((unsigned)(gv[r] >> 32) == ep);
+            const unsigned long long bal = __ballot(ok);
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              run = run && (((bal >> (16 * jj)) & 0xffffull) == 0xffffull);
+              if (run) nb = 4 * r + jj + 1;
+            }
+          }
+          nb = uni(min(nb, Bmax - b + 1));
+        }
+        // ring slots: block x is free once the consumer has passed x - 16
+        if (consv < b + nb - FL_RINGB) consv = uni(lds_vload(cons));
+        nb = min(nb, consv + FL_RINGB - b);
+        if (nb <= 0) {
+          if (k0 == 0 || consv + FL_RINGB <= b) __builtin_amdgcn_s_sleep(1);  // (granule polls pace themselves)
+          if (++spins > FL_SPIN_MAX) { if (lane == 0) atomicExch(a.err, 1); break; }
+          continue;
+        }
+        // codes for the blocks' next phases must be in LDS before they are published
+        if (Yr < L8 && Yr < 16 * (b + nb) + 192) load_codes(16 * (b + nb) + 1024);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int blk = b + 4 * r + (lane >> 4);
+          if (blk < b + nb) *L(ring + (blk & (FL_RINGB - 1)) * 16 + (lane & 15)) = val[r];
+        }
+        FL_CBAR();
+        if (lane == 0) lds_vstore(pub, b + nb);
+        b += nb;
+      }
+    } else if (w == W + 1) {
+      // ============ io-out: links' blocks -> BR (pass 2), last link -> granules ============
+      int bl[W + 1], bmx[W + 1];
+#pragma unroll
+      for (int l = 0; l <= W; ++l) {
+        bl[l] = 0;
+        bmx[l] = (l >= 1 && k0 + l < S && (SAVE || l == W)) ? fl_bmax(k0 + l, m, n) : -1;
+      }
+      unsigned long long* g_out = a.gbuf + (size_t)item * a.gbuf_stride;
+      unsigned spins = 0;
+      for (;;) {
+        bool left = false, any = false;
+#pragma unroll
+        for (int l = 1; l <= W; ++l) {
+          if (bl[l] > bmx[l]) continue;
+          left = true;
+          const int kc = k0 + l;
+          const int avail = min(uni(lds_vload(flags + 32 + l)) - fl_dq(kc), bmx[l] + 1);
+          FL_CBAR();
+          if (avail <= bl[l]) continue;
+          any = true;
+          const int nb = min(4, avail - bl[l]);
+          const int j = lane >> 4, c = lane & 15;
+          if (j < nb) {
+            const int blk = bl[l] + j;
+            const int v = *(const lds_int*)(rings + l * 256 + (blk & (FL_RINGB - 1)) * 16 + c);
+            if (SAVE) a.br[(size_t)(kc - 1) * a.brw + 16 * blk + c] = v;
+            if (l == W) {
+              const int col = fl_cs(kc) + 16 * blk + c;
+              if (col + MSA_GOFF >= 0 && col + MSA_GOFF < a.gbuf_stride)
+                gstore(g_out + col + MSA_GOFF, ((unsigned long long)ep << 32) | (unsigned)v);
+            }
+          }
+          bl[l] += nb;
+          FL_CBAR();
+          if (lane == 0) lds_vstore(flags + 64 + l, bl[l]);
+        }
+        if (!left) break;
+        if (!any) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > FL_SPIN_MAX) { if (lane == 0) atomicExch(a.err, 1); break; }
+        }
+      }
+    } else if (k0 + w < S) {
+      // =================== compute wave: stripe k ===================
+      const int k = k0 + w;
+      const int cs = fl_cs(k);
+      const int P = fl_P(k, m, n);
+      const int row_i = 64 * k + lane + 1;
+      const unsigned ac = (row_i <= m) ? (a.A[pd.a_off + row_i - 1] & 7u) : 0u;
+      const bool has_out = (k < S - 1);
+      const int Bin = (k == 0) ? P - 1 : min(P - 1, fl_bmax(k, m, n));
+      const int dq_in = (w == 0) ? 0 : fl_dq(k);  // producer's counter counts phases (io-in: blocks)
+      const int dq = has_out ? fl_dq(k + 1) : 0;  // phase q writes out block q - dq
+      // LDS byte addresses (32-bit, for the inline-asm DS ops)
+      const unsigned a_ring_in = lds_addr(rings + w * 256);
+      const unsigned a_prog_in = lds_addr(flags + 32 + w);
+      const unsigned a_ring_out = lds_addr(rings + (w + 1) * 256);
+      const unsigned a_prog_me = lds_addr(flags + 32 + w + 1);
+      // out-ring consumers: the next compute wave (or io-out for the last link) and io-out's BR copy
+      const unsigned a_cons1 = lds_addr(w + 1 < W ? flags + 32 + w + 2 : flags + 64 + W);
+      const unsigned a_cons2 = lds_addr(flags + 64 + w + 1);
+      const bool two_cons = SAVE || (w + 1 == W);
+      const unsigned a_dummy = lds_addr(flags + 96 + 8 * (w & 1));  // sink for a phase with nothing to hand off
+      unsigned plo, phi;
+      fl_profile<GS, FLOOR>(kp.match, kp.mismatch, g, ac, plo, phi);
+      // LDS code address: column cs - lane + t, copy x = (cs - lane + OFF) & 7
+      unsigned a_code;
+      {
+        const int c0 = cs - lane + FL_OFF;
+        const int x = c0 & (FL_NCOPY - 1);
+        a_code = lds_addr(reinterpret_cast<int*>(codes + x * L8 + (c0 - x)));
+      }
+      // G-space: H = G - g(i+j), i+j = 64k + 1 + cs + t for every lane of step t
+      const int negct0 = -g * (64 * k + 1 + cs);
+      int gk[16];
+#pragma unroll
+      for (int kx = 0; kx < 16; ++kx) {
+        gk[kx] = -g * kx;
+        if constexpr (BEST) asm("" : "+v"(gk[kx]));  // VGPR constants: H = v_add3(G, -ct_q, -g k)
+      }
+
+      int X = GS ? g * (64 * k + cs) : -g;      // left neighbour at step 0 (virtual cell, H = 0)
+      int U = GS ? g * (64 * k + cs - 1) : -g;  // diagonal at step 0
+      int best = 0;
+      int pubv = 0, consv = 0;
+      unsigned spins = 0;
+      fl_v4i INa[4], INb[4];
+      fl_v4u CWa, CWb;
+      const unsigned long long m63 = 1ull << 63;
+
+      // all LDS traffic of the loop is inline asm with hand-placed waits
+      auto issue_reads = [&](int q, fl_v4i (&IN)[4], fl_v4u& CW, int& pubn) __attribute__((always_inline)) {
+        const unsigned ra = a_ring_in + (unsigned)((q & (FL_RINGB - 1)) * 64);
+        pubn = ds_read_b32(a_prog_in);
+        IN[0] = ds_read_b128<0>(ra);
+        IN[1] = ds_read_b128<16>(ra);
+        IN[2] = ds_read_b128<32>(ra);
+        IN[3] = ds_read_b128<48>(ra);
+        CW = ds_read2_b64(a_code + 16 * q);
+      };
+      auto reread_in = [&](int q, fl_v4i (&IN)[4]) __attribute__((always_inline)) {
+        ds_reread_b128x4(a_ring_in + (unsigned)((q & (FL_RINGB - 1)) * 64), IN);
+      };
+      auto wait_flag = [&](unsigned addr, int& val, int need) __attribute__((always_inline)) {
+        while (val < need) {
+          int v = ds_read_b32(addr);
+          lgkm_wait<0>(v);
+          val = uni(v);
+          if (val < need) {
+            __builtin_amdgcn_s_sleep(0);
+            if (++spins > FL_SPIN_MAX) { if (lane == 0) atomicExch(a.err, 1); break; }
+          }
+        }
+      };
+      auto refresh_cons = [&](int need) __attribute__((always_inline)) {
+        while (consv < need) {
+          int c1 = ds_read_b32(a_cons1);
+          int c2 = ds_read_b32(a_cons2);
+          lgkm_wait<0>(c1);
+          lgkm_wait<0>(c2);
+          consv = uni(two_cons ? min(c1, c2) : c1);
+          if (consv < need) {
+            __builtin_amdgcn_s_sleep(0);
+            if (++spins > FL_SPIN_MAX) { if (lane == 0) atomicExch(a.err, 1); break; }
+          }
+        }
+      };
+      auto mask_in = [&](int q, fl_v4i (&IN)[4]) __attribute__((always_inline)) {
+        if (q > Bin) {  // past the producer's last column (all > n)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) IN[u] = fl_v4i{MSA_NEG, MSA_NEG, MSA_NEG, MSA_NEG};
+        }
+      };
+      // phase 0 inputs, synchronously
+      wait_flag(a_prog_in, pubv, min(1, Bin + 1) + dq_in);
+      {
+        int pub0;
+        issue_reads(0, INa, CWa, pub0);
+        lgkm_wait_v<0>(INa, CWa);
+        lgkm_wait<0>(pub0);
+        mask_in(0, INa);
+      }
+
+      auto run_phase = [&](const int q, fl_v4i (&IN)[4], fl_v4u& CW, fl_v4i (&INn)[4], fl_v4u& CWn, auto MASK_)
+          __attribute__((always_inline)) {
+        constexpr bool MASK = decltype(MASK_)::value;  // phase q+1 may lie past the producer's last block
+        const int need = MASK ? min(q + 1, Bin + 1) : q + 1;
+        FL_STAMP(q, 0, __builtin_amdgcn_s_memtime());
+        FL_STAMP(q, 2, __builtin_amdgcn_s_memrealtime());
+        if (pubv - dq_in < need) {
+          wait_flag(a_prog_in, pubv, need + dq_in);
+          reread_in(q, IN);
+          if constexpr (MASK) mask_in(q, IN);
+        }
+        FL_STAMP(q, 1, __builtin_amdgcn_s_memtime());
+        if constexpr (SAVE) {
+          if (q % FL_PS == 0) {  // pass 2 restarts here: each lane's left and diagonal values
+            int* sp = a.snap + ((size_t)k * a.nseg + q / FL_PS) * 128 + lane;
+            sp[0] = X;
+            sp[64] = U;
+          }
+        }
+        int hv[16], xo[16];
+        int pubn = 0;
+        const int negct = negct0 - 16 * g * q;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const unsigned s4 = __builtin_amdgcn_perm(phi, plo, CW[u]);
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) {
+            const int kx = 4 * u + kk;
+            if (kx == 8) issue_reads(q + 1, INn, CWn, pubn);  // prefetch phase q+1 (6 DS ops)
+            const int s = ((int)(s4 << (24 - 8 * kk))) >> 24;
+            const int h = fl_step<GS, FLOOR>(IN[kx >> 2][kx & 3], s, X, U, g);
+            xo[kx] = X;
+            if constexpr (BEST) hv[kx] = GS ? h + negct + gk[kx] : h;
+          }
+        }
+        if constexpr (BEST) {
+#pragma unroll
+          for (int kx = 0; kx < 16; kx += 2) best = imax3(best, hv[kx], hv[kx + 1]);
+        }
+        lgkm_wait<5>(pubn);  // the counter read (oldest of the six) has landed
+        pubv = uni(pubn);
+        // hand-off: lane 63's 16 values of this phase = block q - dq of the out ring
+        const int bq = q - dq;
+        const bool wr = has_out && bq >= 0;
+        if (wr && consv < bq - (FL_RINGB - 1)) refresh_cons(bq - (FL_RINGB - 1));
+        const unsigned wa = wr ? a_ring_out + (unsigned)((bq & (FL_RINGB - 1)) * 64) : a_dummy;
+        ds_handoff(m63, wa, fl_v4i{xo[0], xo[1], xo[2], xo[3]}, fl_v4i{xo[4], xo[5], xo[6], xo[7]},
+                   fl_v4i{xo[8], xo[9], xo[10], xo[11]}, fl_v4i{xo[12], xo[13], xo[14], xo[15]}, a_prog_me, q + 1);
+        lgkm_wait_v<5>(INn, CWn);  // phase q+1's prefetched inputs have landed (the writes may fly)
+        if constexpr (MASK) mask_in(q + 1, INn);
+      };
+      using T_ = std::true_type;
+      using F_ = std::false_type;
+      // phases q < qa prefetch a block q+1 <= Bin: no masking code
+      const int qa = max(0, min(P, Bin));
+      int q = 0;
+      for (; q + 1 < qa; q += 2) {
+        run_phase(q, INa, CWa, INb, CWb, F_{});
+        run_phase(q + 1, INb, CWb, INa, CWa, F_{});
+      }
+      if (q < qa) {
+        run_phase(q, INa, CWa, INb, CWb, F_{});
+        ++q;
+        for (; q + 1 < P; q += 2) {
+          run_phase(q, INb, CWb, INa, CWa, T_{});
+          run_phase(q + 1, INa, CWa, INb, CWb, T_{});
+        }
+        if (q < P) run_phase(q, INb, CWb, INa, CWa, T_{});
+      } else {
+        for (; q + 1 < P; q += 2) {
+          run_phase(q, INa, CWa, INb, CWb, T_{});
+          run_phase(q + 1, INb, CWb, INa, CWa, T_{});
+        }
+        if (q < P) run_phase(q, INa, CWa, INb, CWb, T_{});
+      }
+      lgkm_wait_v<0>(INa, CWa);
+      lgkm_wait_v<0>(INb, CWb);
+      // ---- stripe finalize ----
+      msa_stripe_meta* md = a.meta + pd.stripe0 + k;
+      if constexpr (BEST) {
+        int bb = (row_i <= m) ? best : INT32_MIN;
+        int bi = row_i;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+          const int ob = __shfl_xor(bb, off);
+          const int oi = __shfl_xor(bi, off);
+          if (ob > bb || (ob == bb && oi < bi)) { bb = ob; bi = oi; }
+        }
+        if (lane == 0) {
+          md->best = bb;
+          md->best_i = bi;
+          md->best_j = -1;
+        }
+      }
+      if (lane == 0) {
+        md->cs = cs;
+        md->phases = P;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Pass 2: block (stripe s, segment seg) of FL_PS phases, one wave each.
+template <bool FLOOR, bool TRACKPOS>
+__global__ __launch_bounds__(256) void fill_kernel(KArgs a) {
+  constexpr bool GS = !FLOOR;
+  const msa_kparams& kp = a.kp;
+  const int lane = threadIdx.x & 63;
+  const int blk = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+  const msa_pair_desc pd = a.pairs[0];
+  const int m = pd.m, n = pd.n, S = (m + 63) / 64, g = kp.gap_ext;
+  const int s = blk / a.nseg, seg = blk - s * a.nseg;
+  int bb = INT32_MIN, bi = 0, bj = 0;
+  if (s < S) {
+    const int P = fl_P(s, m, n);
+    const int q0 = seg * FL_PS;
+    if (q0 < P) {
+      const int q1 = min(P, q0 + FL_PS);
+      const int cs = fl_cs(s);
+      const int row_i = 64 * s + lane + 1;
+      const unsigned ac = (row_i <= m) ? (a.A[pd.a_off + row_i - 1] & 7u) : 0u;
+      unsigned plo, phi;
+      fl_profile<GS, FLOOR>(kp.match, kp.mismatch, g, ac, plo, phi);
+      const int Bin = (s == 0) ? P - 1 : min(P - 1, fl_bmax(s, m, n));
+      const int* sp = a.snap + ((size_t)s * a.nseg + seg) * 128 + lane;
+      int X = sp[0], U = sp[64];
+      const int* brow = a.br + (size_t)(s > 0 ? s - 1 : 0) * a.brw;
+      // column codes: lane r needs columns cs - r + t; column c sits in global copy
+      // (c-1+CPAD)&15 at byte (c-1+CPAD) & ~15: one aligned dwordx4 per phase
+      const int b0 = cs - lane - 1 + MSA_CPAD;
+      const unsigned* cptr = reinterpret_cast<const unsigned*>(a.cod + (size_t)(b0 & (MSA_NCOPY - 1)) * a.cod_copy +
+                                                             pd.cod_off + (b0 & ~(MSA_NCOPY - 1)));
+      const int negct0 = -g * (64 * s + 1 + cs);
+      int gk[16];
+#pragma unroll
+      for (int kx = 0; kx < 16; ++kx) {
+        gk[kx] = -g * kx;
+        asm("" : "+v"(gk[kx]));
+      }
+      int best = INT32_MIN, bt = -1;
+      msa_v4i* hp = reinterpret_cast<msa_v4i*>(a.outH + (size_t)pd.out_off + (size_t)s * pd.pmax * MSA_K * 64) + lane;
+      for (int q = q0; q < q1; ++q) {
+        int IN[16];
+        if (q <= Bin) {
+          if (s == 0) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) IN[j] = GS ? g * (cs + 16 * q + j) : -g;
+          } else {
+            const int4* src = reinterpret_cast<const int4*>(brow + 16 * q);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int4 v = src[u];
+              IN[4 * u] = v.x; IN[4 * u + 1] = v.y; IN[4 * u + 2] = v.z; IN[4 * u + 3] = v.w;
+            }
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 16; ++j) IN[j] = MSA_NEG;
+        }
+        const uint4 c4 = *reinterpret_cast<const uint4*>(cptr + 4 * q);
+        const unsigned cw[4] = {c4.x, c4.y, c4.z, c4.w};
+        const int negct = negct0 - 16 * g * q;
+        int hv[16];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const unsigned s4 = __builtin_amdgcn_perm(phi, plo, cw[u]);
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) {
+            const int kx = 4 * u + kk;
+            const int sc = ((int)(s4 << (24 - 8 * kk))) >> 24;
+            const int h = fl_step<GS, FLOOR>(IN[kx], sc, X, U, g);
+            hv[kx] = GS ? h + negct + gk[kx] : h;
+            if constexpr (TRACKPOS) {
+              if (hv[kx] > best) { best = hv[kx]; bt = 16 * q + kx; }
+            }
+          }
+          __builtin_nontemporal_store(msa_v4i{hv[4 * u], hv[4 * u + 1], hv[4 * u + 2], hv[4 * u + 3]},
+                                      hp + (size_t)(4 * q + u) * 64);
+        }
+        if constexpr (!TRACKPOS) {
+#pragma unroll
+          for (int kx = 0; kx < 16; kx += 2) best = imax3(best, hv[kx], hv[kx + 1]);
+        }
+      }
+      bb = (row_i <= m) ? best : INT32_MIN;
+      bi = row_i;
+      bj = TRACKPOS ? cs + bt - lane : -1;
+    }
+  }
+  // first max in row-major order: max score, then min row, then min column
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const int ob = __shfl_xor(bb, off), oi = __shfl_xor(bi, off), oj = __shfl_xor(bj, off);
+    if (ob > bb || (ob == bb && (oi < bi || (oi == bi && oj < bj)))) { bb = ob; bi = oi; bj = oj; }
+  }
+  if (lane == 0) a.blk[blk] = make_int4(bb, bi, bj, 0);
+}
+
+// Pair result of a two-pass plan from the pass-2 block bests.
+__global__ __launch_bounds__(256) void reduce_blocks_kernel(const int4* blk, int nblk, PairResult* out) {
+  __shared__ int4 sh[256];
+  int b = 0, bi = 0, bj = 0;  // empty alignment: score 0 at (0, 0)
+  auto better = [](int vb, int vi, int vj, int b_, int i_, int j_) {
+    return vb > b_ || (vb == b_ && vb > 0 && (vi < i_ || (vi == i_ && vj < j_)));
+  };
+  for (int x = threadIdx.x; x < nblk; x += 256) {
+    const int4 v = blk[x];
+    if (better(v.x, v.y, v.z, b, bi, bj)) { b = v.x; bi = v.y; bj = v.z; }
+  }
+  sh[threadIdx.x] = make_int4(b, bi, bj, 0);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int x = 1; x < 256; ++x) {
+      const int4 v = sh[x];
+      if (better(v.x, v.y, v.z, b, bi, bj)) { b = v.x; bi = v.y; bj = v.z; }
+    }
+    PairResult r;
+    r.score = b;
+    r.status = 0;
+    r.end_i = bi;
+    r.end_j = bj;
+    r.fin[0] = r.fin[1] = r.fin[2] = 0;
+    r.pad = 0;
+    out[0] = r;
+  }
+}
+
+}  // namespace msa

@@ -138,6 +138,11 @@ struct KArgs {
   const uint8_t* cod;        // MSA_NCOPY byte-shifted copies of the padded column codes (stage_codes_kernel)
   long long cod_copy;        // bytes per copy
   unsigned long long* stamps;  // diagnostic build only (MSA_STAMPS): per-phase s_memtime
+  // two-pass single pair (msa_flow.hip)
+  int32_t* br;    // [S][brw] bottom row of every stripe (pass 1 -> pass 2)
+  int32_t* snap;  // [S][nseg][2][64] lane states at every FL_PS-th phase
+  int4* blk;      // [S * nseg] pass-2 block bests
+  int brw, nseg;
 };
 
 template <int ALG>
@@ -1179,10 +1184,13 @@ struct PairResult {
   int32_t pad;
 };
 
-__global__ void reduce_pairs_kernel(const msa_pair_desc* pairs, const msa_stripe_meta* meta, int n_pairs, int sw,
-                                    PairResult* out) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(64) void reduce_pairs_kernel(const msa_pair_desc* pairs, const msa_stripe_meta* meta,
+                                                         int n_pairs, int sw, PairResult* out) {
+  // one wave per pair: lanes stride over the pair's stripes (a serial loop of
+  // dependent meta loads took ~27 us for a 157-stripe pair)
+  const int p = blockIdx.x;
   if (p >= n_pairs) return;
+  const int lane = threadIdx.x;
   const msa_pair_desc pd = pairs[p];
   const int S = (pd.m + 63) / 64;
   PairResult r;
@@ -1190,10 +1198,17 @@ __global__ void reduce_pairs_kernel(const msa_pair_desc* pairs, const msa_stripe
   r.pad = 0;
   r.fin[0] = r.fin[1] = r.fin[2] = 0;
   if (sw) {
-    int b = 0, bi = 0, bj = 0;  // empty alignment: score 0 at (0,0)
-    for (int s = 0; s < S; ++s) {
-      const msa_stripe_meta md = meta[pd.stripe0 + s];
-      if (md.best > b) { b = md.best; bi = md.best_i; bj = md.best_j; }
+    // first max in row-major order; the empty alignment (score 0 at (0,0))
+    // wins unless some stripe has a positive best
+    int b = 0, bi = 0, bj = 0;
+    for (int s = lane; s < S; s += 64) {
+      const msa_stripe_meta& md = meta[pd.stripe0 + s];
+      if (md.best > b) { b = md.best; bi = md.best_i; bj = md.best_j; }  // strided: rows increase with s
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const int ob = __shfl_xor(b, off), oi = __shfl_xor(bi, off), oj = __shfl_xor(bj, off);
+      if (ob > b || (ob == b && ob > 0 && oi < bi)) { b = ob; bi = oi; bj = oj; }
     }
     r.score = b;
     r.end_i = bi;
@@ -1208,7 +1223,7 @@ __global__ void reduce_pairs_kernel(const msa_pair_desc* pairs, const msa_stripe
     r.end_j = pd.n;
     r.status = md.has_fin ? 0 : -1;
   }
-  out[p] = r;
+  if (lane == 0) out[p] = r;
 }
 
 // ---------------------------------------------------------------------------

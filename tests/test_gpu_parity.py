@@ -85,6 +85,47 @@ def test_sw_linear_single_multi_group(oracle, dev, LB, scoring):
             assert pl.checksum(H) == oracle.checksum_h(o["H"])
 
 
+@pytest.mark.parametrize("scoring", SW_SCORINGS)
+@pytest.mark.parametrize("track_end", [False, True])
+def test_sw_linear_single_score_only(oracle, dev, LB, scoring, track_end):
+    """Single pair, no cell output: the two-pass plan's pass 1 alone keeps the best cell
+    (score only), or the stripe kernel when the end cell is wanted."""
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+
+    ma, mi, g = scoring
+    rng = np.random.default_rng(23)
+    for (m, n) in [(1, 3), (64, 64), (65, 1), (300, 1200), (1300, 700), (2600, 2100)]:
+        A, B = rs(rng, m), rs(rng, n)
+        pl = Plan(LB.SW_LINEAR, LB.CELLS_NONE, [m], [n], [0], [0], match=ma, mismatch=mi, gap_open=g, gap_extend=g,
+                  track_end=track_end, single=True)
+        pl.run(_dev(A, dev), _dev(B, dev))
+        res = pl.results()[0]
+        o = oracle.sw(A, B, ma, mi, g, g)
+        assert res["score"] == o["score"], (m, n)
+        if track_end:
+            assert tuple(res["end"]) == tuple(o["end"]), (m, n)
+
+
+@pytest.mark.parametrize("flow", ["0", "1"])
+def test_sw_linear_single_flow_switch(oracle, dev, LB, monkeypatch, flow):
+    """MSA_FLOW=0 keeps the one-pass stripe kernel for single pairs; both give the oracle's H."""
+    import torch
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+
+    monkeypatch.setenv("MSA_FLOW", flow)
+    rng = np.random.default_rng(29)
+    for (ma, mi, g), (m, n) in [((1, 0, 1), (2100, 1900)), ((2, -1, 1), (1800, 2300))]:
+        A, B = rs(rng, m), rs(rng, n)
+        pl = Plan(LB.SW_LINEAR, LB.CELLS_H, [m], [n], [0], [0], match=ma, mismatch=mi, gap_open=g, gap_extend=g,
+                  track_end=True, single=True)
+        H = torch.empty(pl.cells_elems, dtype=torch.int32, device=dev)
+        pl.run(_dev(A, dev), _dev(B, dev), H)
+        res = pl.results()[0]
+        o = oracle.sw(A, B, ma, mi, g, g, want_h=True)
+        assert (res["score"], tuple(res["end"])) == (o["score"], tuple(o["end"])), (m, n)
+        assert pl.checksum(H) == oracle.checksum_h(o["H"])
+
+
 @pytest.mark.parametrize("scoring", [(2, -1, 1), (1, 0, 1)])
 def test_sw_linear_batch_ragged(oracle, dev, LB, scoring):
     import torch
