@@ -112,16 +112,14 @@ kfn_t pick_kernel(int alg, int out, int tp, bool sgl) {
 }
 
 // single-pair SW linear (msa_flow.hip): pass 1 (chain), pass 2 (fill + H)
-kfn_t pick_flow(int alg, bool best, bool save) {
+kfn_t pick_flow(int alg, bool best, bool save, int tp) {
   const bool fl = (alg == MSA_ALG_SWL);
-  if (best) return fl ? flow_kernel<true, true, false> : flow_kernel<false, true, false>;
-  if (save) return fl ? flow_kernel<true, false, true> : flow_kernel<false, false, true>;
+  if (best) return fl ? flow_kernel<true, true, false, false> : flow_kernel<false, true, false, false>;
+  if (save) {
+    if (fl) return tp ? flow_kernel<true, false, true, true> : flow_kernel<true, false, true, false>;
+    return tp ? flow_kernel<false, false, true, true> : flow_kernel<false, false, true, false>;
+  }
   return nullptr;
-}
-kfn_t pick_fill(int alg, int tp) {
-  const bool fl = (alg == MSA_ALG_SWL);
-  if (fl) return tp ? fill_kernel<true, true> : fill_kernel<true, false>;
-  return tp ? fill_kernel<false, true> : fill_kernel<false, false>;
 }
 
 int env_int(const char* name, int dflt) {
@@ -144,12 +142,12 @@ struct msa_plan {
   int grid = 1;
   int threads = 64;
   bool flow = false;   // flow_kernel (single-pair SW linear) instead of stripe_kernel
-  bool flow2 = false;  // + fill_kernel pass (O_H)
-  kfn_t fn2 = nullptr;
-  int grid2 = 0;
-  int32_t* d_br = nullptr;
-  int32_t* d_snap = nullptr;
+  bool flow2 = false;  // + pass-2 blocks inside the same launch (O_H)
+  unsigned long long* d_br = nullptr;
+  unsigned long long* d_snap = nullptr;
   int4* d_blk = nullptr;
+  int* d_order = nullptr;
+  int nflow = 0;  // two-pass: pass-1 workgroups (the rest of the grid runs pass-2 blocks)
   int brw = 0, nseg = 0, nblk = 0;
   int gbuf_stride = 0;
   kfn_t fn = nullptr;
@@ -268,8 +266,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   const int KS = flow ? 16 : (single ? ks_single(kalg) : MSA_KS_BATCH);
   P->KS = KS;
   P->threads = (flow ? W + 2 : W + 1 + (single ? 1 : 0)) * 64;
-  P->fn = flow ? pick_flow(kalg, out_mode == MSA_OUT_NONE, out_mode == MSA_OUT_H) : pick_kernel(kalg, out_mode, tp, single);
-  if (P->flow2) P->fn2 = pick_fill(kalg, tp);
+  P->fn = flow ? pick_flow(kalg, out_mode == MSA_OUT_NONE, out_mode == MSA_OUT_H, tp) : pick_kernel(kalg, out_mode, tp, single);
   if (!P->fn) { delete P; return MSA_ERR_UNSUPPORTED; }
   P->nc = nc_of(kalg);
   const int band = (kalg == MSA_ALG_NWA) ? desc->band : -1;
@@ -362,6 +359,8 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   if (flow) {
     kp.lds_code_bytes = fl_code_bytes((int)desc->n[0]);
     P->lds_bytes = flow_lds;
+    // pass-2 blocks: 544 ints per wave past the flags
+    if (out_mode == MSA_OUT_H) P->lds_bytes = std::max(flow_lds, (size_t)(FL_FLAGS + (FL_W + 2) * 544) * 4);
   }
   if (P->lds_bytes > 160 * 1024) {
     std::fprintf(stderr, "msa: problem needs %zu B of LDS per workgroup (> 160 KiB)\n", P->lds_bytes);
@@ -392,6 +391,9 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     const int chunk = (kp.n_items + 7) / 8;
     kp.sched_cap = chunk;
     P->grid = 8 * std::max(1, std::min(chunk, per_xcd));
+    // two-pass: the remaining CUs run pass-2 blocks inside the same launch
+    P->nflow = P->grid;
+    if (P->flow2) P->grid = std::max(P->grid + 8, 8 * per_xcd);
   }
   // device buffers
   auto fail = [&](void) { msa_plan_destroy(P); return MSA_ERR_HIP; };
@@ -422,10 +424,23 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     P->brw = 16 * P->pairs[0].pmax + 16;
     P->nseg = (P->pairs[0].pmax + FL_PS - 1) / FL_PS;
     P->nblk = S * P->nseg;
-    P->grid2 = (P->nblk + 3) / 4;
-    if (hipMalloc(&P->d_br, sizeof(int32_t) * (size_t)S * P->brw) != hipSuccess) return fail();
-    if (hipMalloc(&P->d_snap, sizeof(int32_t) * (size_t)P->nblk * 128) != hipSuccess) return fail();
-    if (hipMalloc(&P->d_blk, sizeof(int4) * (size_t)P->grid2 * 4) != hipSuccess) return fail();
+    // pass-2 blocks in expected readiness order: stripe s starts ~6.5 phases after
+    // stripe s-1, and segment seg is complete FL_PS (seg + 1) phases after its start
+    std::vector<int> order(P->nblk);
+    std::vector<double> key(P->nblk);
+    for (int b = 0; b < P->nblk; ++b) {
+      order[b] = b;
+      key[b] = 6.5 * (b / P->nseg) + (double)FL_PS * (b % P->nseg + 1);
+    }
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return key[x] < key[y]; });
+    const size_t brb = sizeof(unsigned long long) * (size_t)S * P->brw;
+    const size_t snb = sizeof(unsigned long long) * (size_t)P->nblk * 128;
+    if (hipMalloc(&P->d_br, brb) != hipSuccess || hipMemset(P->d_br, 0, brb) != hipSuccess) return fail();
+    if (hipMalloc(&P->d_snap, snb) != hipSuccess || hipMemset(P->d_snap, 0, snb) != hipSuccess) return fail();
+    if (hipMalloc(&P->d_blk, sizeof(int4) * (size_t)P->nblk) != hipSuccess) return fail();
+    if (hipMalloc(&P->d_order, sizeof(int) * (size_t)P->nblk) != hipSuccess) return fail();
+    if (hipMemcpy(P->d_order, order.data(), sizeof(int) * (size_t)P->nblk, hipMemcpyHostToDevice) != hipSuccess)
+      return fail();
   }
   if (hipEventCreate(&P->ev0) != hipSuccess || hipEventCreate(&P->ev1) != hipSuccess) return fail();
   *out = P;
@@ -445,6 +460,7 @@ void msa_plan_destroy(msa_plan* P) {
   if (P->d_br) (void)hipFree(P->d_br);
   if (P->d_snap) (void)hipFree(P->d_snap);
   if (P->d_blk) (void)hipFree(P->d_blk);
+  if (P->d_order) (void)hipFree(P->d_order);
   if (P->ev0) (void)hipEventDestroy(P->ev0);
   if (P->ev1) (void)hipEventDestroy(P->ev1);
   delete P;
@@ -496,8 +512,11 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
   a.br = P->d_br;
   a.snap = P->d_snap;
   a.blk = P->d_blk;
+  a.border = P->d_order;
+  a.nflow = P->nflow;
   a.brw = P->brw;
   a.nseg = P->nseg;
+  a.nblk = env_int("MSA_NOFILL", 0) ? 0 : P->nblk;  // (diagnostic: pass 1 alone)
   HIPCHK(hipMemsetAsync(P->d_ticket, 0, 64, st));
   {
     const unsigned virt = (P->kp.alg == MSA_ALG_SWL || P->kp.alg == MSA_ALG_SWL0 || P->kp.alg == MSA_ALG_SWA) ? MSA_VIRT_CODE : 0u;
@@ -508,10 +527,6 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
   HIPCHK(hipEventRecord(P->ev0, st));
   hipLaunchKernelGGL(P->fn, dim3(P->grid), dim3(P->threads), P->lds_bytes, st, a);
   HIPCHK(hipGetLastError());
-  if (P->flow2) {
-    hipLaunchKernelGGL(P->fn2, dim3(P->grid2), dim3(256), 0, st, a);
-    HIPCHK(hipGetLastError());
-  }
   HIPCHK(hipEventRecord(P->ev1, st));
   if (P->flow2) {
     hipLaunchKernelGGL(reduce_blocks_kernel, dim3(1), dim3(256), 0, st, (const int4*)P->d_blk, P->nblk, P->d_res);
@@ -545,7 +560,10 @@ int msa_plan_results(msa_plan* P, msa_pair_result* out, void* stream) {
   HIPCHK(hipMemcpyAsync(out, P->d_res, sizeof(PairResult) * P->d.n_pairs, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   static_assert(sizeof(PairResult) == sizeof(msa_pair_result), "result layout");
-  if (err[1]) return MSA_ERR_TIMEOUT;
+  if (err[1]) {
+    std::fprintf(stderr, "msa: a kernel wait hit its spin limit (site %d)\n", err[1]);
+    return MSA_ERR_TIMEOUT;
+  }
   return MSA_OK;
 }
 

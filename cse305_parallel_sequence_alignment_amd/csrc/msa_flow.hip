@@ -46,7 +46,17 @@ namespace msa {
 #define FL_NCOPY 8      // byte-shifted LDS code copies (8-byte aligned 8-code reads)
 #define FL_FLAGS 128    // ints of flags at the start of LDS
 #define FL_PS 32        // phases per pass-2 segment (pass 1 saves its state every FL_PS phases)
-#define FL_SPIN_MAX (1u << 26)
+#ifdef FL_DBG
+#define FL_SPIN_MAX (1u << 16)
+#else
+#define FL_SPIN_MAX (1u << 26)  // a spin limit sets err = the site's code (10..15) instead of hanging
+#endif
+#ifndef FL_PF
+#define FL_PF 8         // step of a phase at which the next phase's inputs are read
+#endif
+#ifndef FL_IOSLEEP
+#define FL_IOSLEEP 1    // s_sleep of an idle io wave
+#endif
 
 __host__ __device__ __forceinline__ int fl_cs(int k) { return -((16 - (k & 15)) & 15); }  // -((-k) mod 16)
 __host__ __device__ __forceinline__ int fl_P(int k, int m, int n) {
@@ -71,8 +81,19 @@ __device__ __forceinline__ lds_int* L(int* p) { return (lds_int*)(p); }
 __device__ __forceinline__ int lds_vload(const int* p) { return *(volatile lds_int*)(p); }
 __device__ __forceinline__ void lds_vstore(int* p, int v) { *(volatile lds_int*)(p) = v; }
 #define FL_CBAR() asm volatile("" ::: "memory")
-// Diagnostic build (-DMSA_STAMPS): stamps[((item*16 + w)*4096 + q)*4 + slot]
-//   slot 0: s_memtime at phase start, 1: after its input wait, 2: s_memrealtime at phase start
+// Diagnostic build (-DMSA_STAMPS): stamps[((item*16 + w)*4096 + q)*4 + slot], q = 0:
+//   slot 0: s_memrealtime at the stripe's start, 1: at its end, 2: slow-path phases
+#if defined(MSA_STAMPS) && defined(FL_DBG)
+// live progress probe into host-mapped memory: [block][wave][field]
+#define FL_PROBE(f_, v_)                                                                                   \
+  do {                                                                                                     \
+    if (a.stamps && lane == __builtin_amdgcn_readfirstlane(lane))                                         \
+      __hip_atomic_store(a.stamps + ((size_t)blockIdx.x * 8 + (threadIdx.x >> 6)) * 4 + (f_),              \
+                         (unsigned long long)(v_), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);           \
+  } while (0)
+#else
+#define FL_PROBE(f_, v_) do {} while (0)
+#endif
 #ifdef MSA_STAMPS
 #define FL_STAMP(q_, slot_, v_)                                                                        \
   do {                                                                                              \
@@ -175,7 +196,24 @@ __device__ __forceinline__ int fl_step(int in, int s, int& X, int& U, int g) {
 // FLOOR: scores may be negative (zero floor, X-space); otherwise G-space.
 // BEST: track the best cell in pass 1 (score-only plans: no pass 2).
 // SAVE: write BR and SNAP for pass 2.
-template <bool FLOOR, bool BEST, bool SAVE>
+// What a pass-2 block needs, by value (a reference to the kernel's KArgs would
+// put them on the stack of the pass-1 path too).
+struct FillArgs {
+  const uint8_t* A;
+  const uint8_t* cod;
+  const unsigned long long* br;
+  const unsigned long long* snap;
+  int32_t* outH;
+  int4* blk;
+  int* err;
+  long long cod_copy, a_off, cod_off, out_off;
+  int m, n, pmax, nseg, brw, match, mismatch, g;
+  unsigned ep;
+};
+template <bool FLOOR, bool TRACKPOS>
+__device__ __attribute__((noinline)) void fill_block(const FillArgs f, int blk, int lane, int* lds);
+
+template <bool FLOOR, bool BEST, bool SAVE, bool TRACKPOS>
 __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
   constexpr bool GS = !FLOOR;
   extern __shared__ __attribute__((aligned(16))) int smem[];
@@ -197,14 +235,48 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
   const unsigned ep = kp.epoch;
   const int grp = (int)(blockIdx.x & 7), chunk = kp.sched_cap;
 
+  if constexpr (SAVE) {
+    if ((int)blockIdx.x >= a.nflow) {
+      // pass-2 workgroup: every wave takes blocks on its own, in expected readiness
+      // order.  Workgroups are dispatched in index order, so the pass-1 workgroups
+      // (the lowest indices) are resident before any of these waits on them.
+      for (;;) {
+        // (a separate, non-inlined block function keeps this loop's control flow
+        // uniform: inlined, the structurizer re-entered it without the ticket)
+        int t = 0;
+        if (lane == 0) t = atomicAdd(a.ticket + 12, 1);
+        t = __builtin_amdgcn_readlane(t, 0);
+        FL_PROBE(0, 2000 + t);
+        if (t >= a.nblk) break;
+        const FillArgs f{a.A, a.cod, a.br, a.snap, a.outH, a.blk, a.err, a.cod_copy, a.pairs[0].a_off,
+                         a.pairs[0].cod_off, a.pairs[0].out_off, a.pairs[0].m, a.pairs[0].n, a.pairs[0].pmax,
+                         a.nseg, a.brw, kp.match, kp.mismatch, kp.gap_ext, kp.epoch};
+        fill_block<FLOOR, TRACKPOS>(f, a.border[t], lane, smem + w * 544);
+      }
+      return;
+    }
+  }
+
   for (;;) {
     if (threadIdx.x == 0) {
-      const int t = atomicAdd(a.ticket + 4 + grp, 1);
-      flags[0] = (t < chunk) ? min(grp * chunk + t, kp.n_items) : kp.n_items;
+      // own chunk first, then the others': every item is claimed by a running
+      // workgroup before any workgroup turns to pass-2 blocks (which wait on items)
+      int it = kp.n_items;
+      for (int d = 0; d < 8; ++d) {
+        const int gg = (grp + d) & 7;
+        if (gg * chunk >= kp.n_items) continue;
+        const int t = atomicAdd(a.ticket + 4 + gg, 1);
+        if (t < chunk && gg * chunk + t < kp.n_items) {
+          it = gg * chunk + t;
+          break;
+        }
+      }
+      flags[0] = it;
     }
     if (threadIdx.x >= 16 && threadIdx.x < 128) flags[threadIdx.x] = 0;
     __syncthreads();
     const int item = uni(flags[0]);
+    FL_PROBE(0, 1000 + item);
     if (item >= kp.n_items) break;
     const int k0 = item * W;
 
@@ -238,7 +310,11 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         }
         Yr = max(Yr, Y1);
       };
+#ifdef FL_PRELOAD
+      load_codes(L8);
+#else
       load_codes(1024);
+#endif
       const unsigned long long* g_in = a.gbuf + (size_t)(item > 0 ? item - 1 : 0) * a.gbuf_stride;
       int b = 0;
       int consv = 0;
@@ -282,8 +358,8 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         if (consv < b + nb - FL_RINGB) consv = uni(lds_vload(cons));
         nb = min(nb, consv + FL_RINGB - b);
         if (nb <= 0) {
-          if (k0 == 0 || consv + FL_RINGB <= b) __builtin_amdgcn_s_sleep(1);  // (granule polls pace themselves)
-          if (++spins > FL_SPIN_MAX) { if (lane == 0) atomicExch(a.err, 1); break; }
+          if (k0 == 0 || consv + FL_RINGB <= b) __builtin_amdgcn_s_sleep(FL_IOSLEEP);  // (granule polls pace themselves)
+          if (++spins > FL_SPIN_MAX) { if (lane == 0) atomicExch(a.err, 10); break; }
           continue;
         }
         // codes for the blocks' next phases must be in LDS before they are published
@@ -323,7 +399,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
           if (j < nb) {
             const int blk = bl[l] + j;
             const int v = *(const lds_int*)(rings + l * 256 + (blk & (FL_RINGB - 1)) * 16 + c);
-            if (SAVE) a.br[(size_t)(kc - 1) * a.brw + 16 * blk + c] = v;
+            if (SAVE) gstore(a.br + (size_t)(kc - 1) * a.brw + 16 * blk + c, ((unsigned long long)ep << 32) | (unsigned)v);
             if (l == W) {
               const int col = fl_cs(kc) + 16 * blk + c;
               if (col + MSA_GOFF >= 0 && col + MSA_GOFF < a.gbuf_stride)
@@ -336,8 +412,8 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         }
         if (!left) break;
         if (!any) {
-          __builtin_amdgcn_s_sleep(1);
-          if (++spins > FL_SPIN_MAX) { if (lane == 0) atomicExch(a.err, 1); break; }
+          __builtin_amdgcn_s_sleep(FL_IOSLEEP);
+          if (++spins > FL_SPIN_MAX) { if (lane == 0) atomicExch(a.err, 11); break; }
         }
       }
     } else if (k0 + w < S) {
@@ -408,7 +484,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
           val = uni(v);
           if (val < need) {
             __builtin_amdgcn_s_sleep(0);
-            if (++spins > FL_SPIN_MAX) { if (lane == 0) atomicExch(a.err, 1); break; }
+            if (++spins > FL_SPIN_MAX) { if (lane == 0) atomicExch(a.err, 12); break; }
           }
         }
       };
@@ -421,7 +497,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
           consv = uni(two_cons ? min(c1, c2) : c1);
           if (consv < need) {
             __builtin_amdgcn_s_sleep(0);
-            if (++spins > FL_SPIN_MAX) { if (lane == 0) atomicExch(a.err, 1); break; }
+            if (++spins > FL_SPIN_MAX) { if (lane == 0) atomicExch(a.err, 13); break; }
           }
         }
       };
@@ -431,8 +507,12 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
           for (int u = 0; u < 4; ++u) IN[u] = fl_v4i{MSA_NEG, MSA_NEG, MSA_NEG, MSA_NEG};
         }
       };
+#ifdef MSA_STAMPS
+      int nslow = 0;
+#endif
       // phase 0 inputs, synchronously
       wait_flag(a_prog_in, pubv, min(1, Bin + 1) + dq_in);
+      FL_STAMP(0, 0, __builtin_amdgcn_s_memrealtime());
       {
         int pub0;
         issue_reads(0, INa, CWa, pub0);
@@ -445,19 +525,20 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
           __attribute__((always_inline)) {
         constexpr bool MASK = decltype(MASK_)::value;  // phase q+1 may lie past the producer's last block
         const int need = MASK ? min(q + 1, Bin + 1) : q + 1;
-        FL_STAMP(q, 0, __builtin_amdgcn_s_memtime());
-        FL_STAMP(q, 2, __builtin_amdgcn_s_memrealtime());
+        FL_PROBE(2, q);
         if (pubv - dq_in < need) {
+#ifdef MSA_STAMPS
+          ++nslow;
+#endif
           wait_flag(a_prog_in, pubv, need + dq_in);
           reread_in(q, IN);
           if constexpr (MASK) mask_in(q, IN);
         }
-        FL_STAMP(q, 1, __builtin_amdgcn_s_memtime());
         if constexpr (SAVE) {
           if (q % FL_PS == 0) {  // pass 2 restarts here: each lane's left and diagonal values
-            int* sp = a.snap + ((size_t)k * a.nseg + q / FL_PS) * 128 + lane;
-            sp[0] = X;
-            sp[64] = U;
+            unsigned long long* sp = a.snap + ((size_t)k * a.nseg + q / FL_PS) * 128 + lane;
+            gstore(sp, ((unsigned long long)ep << 32) | (unsigned)X);
+            gstore(sp + 64, ((unsigned long long)ep << 32) | (unsigned)U);
           }
         }
         int hv[16], xo[16];
@@ -469,7 +550,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
 #pragma unroll
           for (int kk = 0; kk < 4; ++kk) {
             const int kx = 4 * u + kk;
-            if (kx == 8) issue_reads(q + 1, INn, CWn, pubn);  // prefetch phase q+1 (6 DS ops)
+            if (kx == FL_PF) issue_reads(q + 1, INn, CWn, pubn);  // prefetch phase q+1 (6 DS ops)
             const int s = ((int)(s4 << (24 - 8 * kk))) >> 24;
             const int h = fl_step<GS, FLOOR>(IN[kx >> 2][kx & 3], s, X, U, g);
             xo[kx] = X;
@@ -489,6 +570,9 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         const unsigned wa = wr ? a_ring_out + (unsigned)((bq & (FL_RINGB - 1)) * 64) : a_dummy;
         ds_handoff(m63, wa, fl_v4i{xo[0], xo[1], xo[2], xo[3]}, fl_v4i{xo[4], xo[5], xo[6], xo[7]},
                    fl_v4i{xo[8], xo[9], xo[10], xo[11]}, fl_v4i{xo[12], xo[13], xo[14], xo[15]}, a_prog_me, q + 1);
+#ifdef MSA_STAMPS
+        if (q == dq) FL_STAMP(0, 3, __builtin_amdgcn_s_memrealtime());
+#endif
         lgkm_wait_v<5>(INn, CWn);  // phase q+1's prefetched inputs have landed (the writes may fly)
         if constexpr (MASK) mask_in(q + 1, INn);
       };
@@ -518,6 +602,9 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
       }
       lgkm_wait_v<0>(INa, CWa);
       lgkm_wait_v<0>(INb, CWb);
+      FL_STAMP(0, 1, __builtin_amdgcn_s_memrealtime());
+      FL_PROBE(1, 7777);
+      FL_STAMP(0, 2, (unsigned long long)nslow);
       // ---- stripe finalize ----
       msa_stripe_meta* md = a.meta + pd.stripe0 + k;
       if constexpr (BEST) {
@@ -540,40 +627,79 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         md->phases = P;
       }
     }
+    FL_PROBE(1, 8888);
     __syncthreads();
   }
+  FL_PROBE(1, 9999);
 }
 
-// Pass 2: block (stripe s, segment seg) of FL_PS phases, one wave each.
+// Pass 2: block (stripe s, segment seg) of FL_PS phases, one wave.  Its inputs
+// are {epoch, value} granules that pass 1 may still be writing: the wave waits
+// for the block's last bottom-row granule, then loads and checks them all.
 template <bool FLOOR, bool TRACKPOS>
-__global__ __launch_bounds__(256) void fill_kernel(KArgs a) {
+__device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, int lane, int* lds) {
   constexpr bool GS = !FLOOR;
-  const msa_kparams& kp = a.kp;
-  const int lane = threadIdx.x & 63;
-  const int blk = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
-  const msa_pair_desc pd = a.pairs[0];
-  const int m = pd.m, n = pd.n, S = (m + 63) / 64, g = kp.gap_ext;
+  const unsigned ep = a.ep;
+  const int m = a.m, n = a.n, S = (m + 63) / 64, g = a.g;
   const int s = blk / a.nseg, seg = blk - s * a.nseg;
   int bb = INT32_MIN, bi = 0, bj = 0;
+#if defined(FL_EXP) && FL_EXP == 1
+  return;
+#endif
   if (s < S) {
     const int P = fl_P(s, m, n);
     const int q0 = seg * FL_PS;
     if (q0 < P) {
-      const int q1 = min(P, q0 + FL_PS);
+      int q1 = min(P, q0 + FL_PS);
       const int cs = fl_cs(s);
       const int row_i = 64 * s + lane + 1;
-      const unsigned ac = (row_i <= m) ? (a.A[pd.a_off + row_i - 1] & 7u) : 0u;
+      const unsigned ac = (row_i <= m) ? (a.A[a.a_off + row_i - 1] & 7u) : 0u;
       unsigned plo, phi;
-      fl_profile<GS, FLOOR>(kp.match, kp.mismatch, g, ac, plo, phi);
+      fl_profile<GS, FLOOR>(a.match, a.mismatch, g, ac, plo, phi);
       const int Bin = (s == 0) ? P - 1 : min(P - 1, fl_bmax(s, m, n));
-      const int* sp = a.snap + ((size_t)s * a.nseg + seg) * 128 + lane;
-      int X = sp[0], U = sp[64];
-      const int* brow = a.br + (size_t)(s > 0 ? s - 1 : 0) * a.brw;
+      const unsigned long long* sp = a.snap + ((size_t)s * a.nseg + seg) * 128 + lane;
+      const unsigned long long* brow = a.br + (size_t)(s > 0 ? s - 1 : 0) * a.brw;
+      // bottom-row blocks [q0, qb) of the row above come from pass 1 (s > 0)
+      const int qb = (s > 0) ? min(q1, Bin + 1) : q0;
+      const int nv = 16 * max(0, qb - q0);  // granules, lane l holds l, l+64, ...
+      int X = 0, U = 0;
+      // uniform waits (ballots) and no early exits: the compiler keeps the wave whole
+      bool ready = (nv == 0);
+      for (int t2 = 0; !ready && t2 < (int)(FL_SPIN_MAX >> 2); ++t2) {  // the block's last granule first
+        const unsigned long long gl = gload(brow + 16 * q0 + nv - 1);
+        ready = __ballot((unsigned)(gl >> 32) != ep) == 0;
+        if (!ready) __builtin_amdgcn_s_sleep(32);
+      }
+      if (ready) {
+        ready = false;
+        for (int tries = 0; !ready && tries < (int)FL_SPIN_MAX; ++tries) {
+          const unsigned long long x0 = gload(sp), u0 = gload(sp + 64);
+          bool ok = ((unsigned)(x0 >> 32) == ep) && ((unsigned)(u0 >> 32) == ep);
+          X = (int)(unsigned)x0;
+          U = (int)(unsigned)u0;
+          for (int v = lane; v < nv; v += 64) {
+            const unsigned long long gv = gload(brow + 16 * q0 + v);
+            ok = ok && ((unsigned)(gv >> 32) == ep);
+            *L(lds + v) = (int)(unsigned)gv;
+          }
+          ready = __ballot(!ok) == 0;
+          if (!ready) __builtin_amdgcn_s_sleep(8);
+        }
+      }
+      if (!ready) {
+        if (lane == 0) atomicExch(a.err, 15);
+        q1 = q0;  // nothing computed; the block reports no cell
+      }
+      FL_CBAR();  // (one wave's LDS ops execute in order: the reads below see the writes)
+#if defined(FL_EXP) && FL_EXP == 2
+      if (lane == 0) a.blk[blk] = make_int4(X, U, 0, 0);
+      return;
+#endif
       // column codes: lane r needs columns cs - r + t; column c sits in global copy
       // (c-1+CPAD)&15 at byte (c-1+CPAD) & ~15: one aligned dwordx4 per phase
       const int b0 = cs - lane - 1 + MSA_CPAD;
       const unsigned* cptr = reinterpret_cast<const unsigned*>(a.cod + (size_t)(b0 & (MSA_NCOPY - 1)) * a.cod_copy +
-                                                             pd.cod_off + (b0 & ~(MSA_NCOPY - 1)));
+                                                             a.cod_off + (b0 & ~(MSA_NCOPY - 1)));
       const int negct0 = -g * (64 * s + 1 + cs);
       int gk[16];
 #pragma unroll
@@ -582,7 +708,7 @@ __global__ __launch_bounds__(256) void fill_kernel(KArgs a) {
         asm("" : "+v"(gk[kx]));
       }
       int best = INT32_MIN, bt = -1;
-      msa_v4i* hp = reinterpret_cast<msa_v4i*>(a.outH + (size_t)pd.out_off + (size_t)s * pd.pmax * MSA_K * 64) + lane;
+      msa_v4i* hp = reinterpret_cast<msa_v4i*>(a.outH + (size_t)a.out_off + (size_t)s * a.pmax * MSA_K * 64) + lane;
       for (int q = q0; q < q1; ++q) {
         int IN[16];
         if (q <= Bin) {
@@ -590,10 +716,10 @@ __global__ __launch_bounds__(256) void fill_kernel(KArgs a) {
 #pragma unroll
             for (int j = 0; j < 16; ++j) IN[j] = GS ? g * (cs + 16 * q + j) : -g;
           } else {
-            const int4* src = reinterpret_cast<const int4*>(brow + 16 * q);
+            const lds_int4* src = reinterpret_cast<const lds_int4*>(L(lds + 16 * (q - q0)));
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-              const int4 v = src[u];
+              const fl_v4i v = src[u];
               IN[4 * u] = v.x; IN[4 * u + 1] = v.y; IN[4 * u + 2] = v.z; IN[4 * u + 3] = v.w;
             }
           }

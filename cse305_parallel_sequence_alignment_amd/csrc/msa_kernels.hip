@@ -139,10 +139,13 @@ struct KArgs {
   long long cod_copy;        // bytes per copy
   unsigned long long* stamps;  // diagnostic build only (MSA_STAMPS): per-phase s_memtime
   // two-pass single pair (msa_flow.hip)
-  int32_t* br;    // [S][brw] bottom row of every stripe (pass 1 -> pass 2)
-  int32_t* snap;  // [S][nseg][2][64] lane states at every FL_PS-th phase
-  int4* blk;      // [S * nseg] pass-2 block bests
-  int brw, nseg;
+  // {epoch, value} granules: pass-2 blocks run while pass 1 is still producing
+  unsigned long long* br;    // [S][brw] bottom row of every stripe
+  unsigned long long* snap;  // [S][nseg][2][64] lane states at every FL_PS-th phase
+  int4* blk;                 // [S * nseg] pass-2 block bests
+  const int* border;         // pass-2 blocks in expected readiness order
+  int brw, nseg, nblk;
+  int nflow;                 // workgroups [0, nflow) run pass 1, the rest pass-2 blocks
 };
 
 template <int ALG>
