@@ -225,7 +225,7 @@ def main():
         traffic = load_traffic(wl)
         roof = dict(bound="hbm", achieved=round(achieved, 2), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
-                    note="algorithmic bytes = %.0f B/cell x cells / stripe-kernel time; the kernel is bound by the "
+                    note="algorithmic bytes = %.0f B/cell x cells / DP-kernel time (flow_kernel for C2); bound by the "
                          "per-wave DP dependency chain of the anti-diagonal wavefront, not by HBM (DESIGN.md)"
                          % algo_bytes_per_cell)
         cpu = None

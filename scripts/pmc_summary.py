@@ -16,6 +16,9 @@ from collections import defaultdict
 from pathlib import Path
 
 src, wl, rnd = Path(sys.argv[1]), sys.argv[2], sys.argv[3]
+# the DP kernel of the workload: flow_kernel (single-pair SW linear, pass 1 + pass-2
+# blocks in one launch) or stripe_kernel (everything else)
+KERNELS = ("flow_kernel", "stripe_kernel")
 dst = Path(__file__).resolve().parent.parent / "profiles"
 dst.mkdir(exist_ok=True)
 
@@ -26,13 +29,13 @@ def per_dispatch(sub):
         return {}
     acc = defaultdict(lambda: defaultdict(float))
     for r in csv.DictReader(open(f)):
-        if "stripe_kernel" not in r["Kernel_Name"]:
+        if not any(k in r["Kernel_Name"] for k in KERNELS):
             continue
         acc[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
     return {k: sum(v.values()) / len(v) for k, v in acc.items()}
 
 
-out = {"workload": wl, "round": rnd, "kernel": "stripe_kernel", "per_launch": {}}
+out = {"workload": wl, "round": rnd, "kernel": "/".join(KERNELS), "per_launch": {}}
 for sub in ("pmc1", "pmc2", "pmc_fetch", "pmc_write"):
     out["per_launch"].update(per_dispatch(sub))
 pl = out["per_launch"]
@@ -44,7 +47,7 @@ stats = src / "trace" / "run_kernel_stats.csv"
 if stats.exists():
     shutil.copy(stats, dst / f"{rnd}_{wl}_kernel_stats.csv")
     for r in csv.DictReader(open(stats)):
-        if "stripe_kernel" in r["Name"]:
+        if any(k in r["Name"] for k in KERNELS):
             out["trace_avg_ns"] = float(r["AverageNs"])
             out["trace_calls"] = int(r["Calls"])
 (dst / f"{rnd}_{wl}_pmc.json").write_text(json.dumps(out, indent=1))
