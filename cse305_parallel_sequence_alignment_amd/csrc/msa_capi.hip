@@ -112,9 +112,13 @@ kfn_t pick_kernel(int alg, int out, int tp, bool sgl) {
 }
 
 // single-pair SW linear (msa_flow.hip): pass 1 (chain), pass 2 (fill + H)
-kfn_t pick_flow(int alg, bool best, bool save, int tp) {
+kfn_t pick_flow(int alg, bool best, bool save, int tp, int R) {
   const bool fl = (alg == MSA_ALG_SWL);
   if (best) return fl ? flow_kernel<true, true, false, false> : flow_kernel<false, true, false, false>;
+  if (save && R == 2) {
+    if (fl) return tp ? flow_kernel<true, false, true, true, 2> : flow_kernel<true, false, true, false, 2>;
+    return tp ? flow_kernel<false, false, true, true, 2> : flow_kernel<false, false, true, false, 2>;
+  }
   if (save) {
     if (fl) return tp ? flow_kernel<true, false, true, true> : flow_kernel<true, false, true, false>;
     return tp ? flow_kernel<false, false, true, true> : flow_kernel<false, false, true, false>;
@@ -147,6 +151,7 @@ struct msa_plan {
   unsigned long long* d_snap = nullptr;
   int4* d_blk = nullptr;
   int* d_order = nullptr;
+  int R = 1;      // flow kernel rows per lane
   int nflow = 0;  // two-pass: pass-1 workgroups (the rest of the grid runs pass-2 blocks)
   int brw = 0, nseg = 0, nblk = 0;
   int gbuf_stride = 0;
@@ -266,7 +271,10 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   const int KS = flow ? 16 : (single ? ks_single(kalg) : MSA_KS_BATCH);
   P->KS = KS;
   P->threads = (flow ? W + 2 : W + 1 + (single ? 1 : 0)) * 64;
-  P->fn = flow ? pick_flow(kalg, out_mode == MSA_OUT_NONE, out_mode == MSA_OUT_H, tp) : pick_kernel(kalg, out_mode, tp, single);
+  // rows per lane of the flow kernel (two-pass plans): 2 halves the inter-wave hand-offs per row
+  P->R = (flow && out_mode == MSA_OUT_H) ? std::max(1, std::min(2, env_int("MSA_R", 2))) : 1;
+  P->fn = flow ? pick_flow(kalg, out_mode == MSA_OUT_NONE, out_mode == MSA_OUT_H, tp, P->R)
+               : pick_kernel(kalg, out_mode, tp, single);
   if (!P->fn) { delete P; return MSA_ERR_UNSUPPORTED; }
   P->nc = nc_of(kalg);
   const int band = (kalg == MSA_ALG_NWA) ? desc->band : -1;
@@ -311,6 +319,10 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
       stripe_geom(k, (int)m, (int)n, band, g, KS);
       pmax = std::max(pmax, g.P * (KS / MSA_K));  // in 16-step layout blocks
     }
+    if (flow) {  // the flow kernels' own geometry (R rows per lane)
+      const int SR = (int)((m + 64 * P->R - 1) / (64 * P->R));
+      for (int k = 0; k < SR; ++k) pmax = std::max(pmax, fl_P(k, (int)m, (int)n, P->R));
+    }
     msa_pair_desc& pd = P->pairs[p];
     pd.a_off = desc->a_off[p];
     pd.b_off = desc->b_off[p];
@@ -334,7 +346,9 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
       }
       pd.cod_off = it->second;
     }
-    const int64_t cells = (int64_t)S * pmax * MSA_K * 64;
+    // R = 2 layout: (m+127)/128 stripes of pmax * 2048 cells
+    const int64_t cells = std::max((int64_t)S * pmax * MSA_K * 64,
+                                   (int64_t)((m + 64 * P->R - 1) / (64 * P->R)) * pmax * MSA_K * 64 * P->R);
     off += (cells + 63) & ~int64_t(63);
     stripe0 += S;
     max_S = std::max(max_S, S);
@@ -347,7 +361,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   P->cod_copy = cod_bytes;
   kp.lds_row_words = single ? 0 : (((max_P * MSA_K + MSA_ROWOFF + 32) + 15) & ~15);
   if (single) {
-    const int S = (int)((desc->m[0] + 63) / 64);
+    const int S = (int)((desc->m[0] + 64 * P->R - 1) / (64 * P->R));
     kp.n_items = (S + W - 1) / W;
   } else {
     kp.n_items = (int)desc->n_pairs;
@@ -420,7 +434,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     if (hipMemset(P->d_gbuf, 0, gb) != hipSuccess) return fail();
   }
   if (P->flow2) {
-    const int S = (int)((desc->m[0] + 63) / 64);
+    const int S = (int)((desc->m[0] + 64 * P->R - 1) / (64 * P->R));
     P->brw = 16 * P->pairs[0].pmax + 16;
     P->nseg = (P->pairs[0].pmax + FL_PS - 1) / FL_PS;
     P->nblk = S * P->nseg;
@@ -430,11 +444,11 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     std::vector<double> key(P->nblk);
     for (int b = 0; b < P->nblk; ++b) {
       order[b] = b;
-      key[b] = 6.5 * (b / P->nseg) + (double)FL_PS * (b % P->nseg + 1);
+      key[b] = (P->R == 2 ? 7.5 : 6.5) * (b / P->nseg) + (double)FL_PS * (b % P->nseg + 1);
     }
     std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return key[x] < key[y]; });
     const size_t brb = sizeof(unsigned long long) * (size_t)S * P->brw;
-    const size_t snb = sizeof(unsigned long long) * (size_t)P->nblk * 128;
+    const size_t snb = sizeof(unsigned long long) * (size_t)P->nblk * 128 * P->R;
     if (hipMalloc(&P->d_br, brb) != hipSuccess || hipMemset(P->d_br, 0, brb) != hipSuccess) return fail();
     if (hipMalloc(&P->d_snap, snb) != hipSuccess || hipMemset(P->d_snap, 0, snb) != hipSuccess) return fail();
     if (hipMalloc(&P->d_blk, sizeof(int4) * (size_t)P->nblk) != hipSuccess) return fail();
@@ -480,7 +494,7 @@ int msa_plan_pair_layout(const msa_plan* P, int64_t pair, int64_t* out4) {
   out4[0] = pd.stripe0;
   out4[1] = pd.pmax;
   out4[2] = pd.out_off;
-  out4[3] = P->KS;
+  out4[3] = P->KS | ((int64_t)P->R << 16);  // bits 16+: rows per lane of the layout (0 = 1)
   return MSA_OK;
 }
 
@@ -581,7 +595,7 @@ int msa_plan_checksum(msa_plan* P, const int32_t* dH, int64_t pair, uint64_t* di
   hipStream_t st = (hipStream_t)stream;
   HIPCHK(hipMemsetAsync(P->d_sum, 0, 8, st));
   hipLaunchKernelGGL(checksum_kernel, dim3(1024), dim3(256), 0, st, dH, P->d_pairs, P->d_meta, (int)pair,
-                     P->kp.band, P->d_sum);
+                     P->kp.band, P->R, P->d_sum);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(digest, P->d_sum, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));

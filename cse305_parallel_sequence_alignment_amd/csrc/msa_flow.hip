@@ -59,15 +59,19 @@ namespace msa {
 #endif
 
 __host__ __device__ __forceinline__ int fl_cs(int k) { return -((16 - (k & 15)) & 15); }  // -((-k) mod 16)
-__host__ __device__ __forceinline__ int fl_P(int k, int m, int n) {
-  const int rlast = (m - 64 * k - 1 < 63) ? (m - 64 * k - 1) : 63;
+// R rows per lane: stripe k holds rows 64Rk+1 .. 64R(k+1); rlast = last lane with a row
+__host__ __device__ __forceinline__ int fl_P(int k, int m, int n, int R = 1) {
+  const int rl = (m - 64 * R * k - 1) / R;
+  const int rlast = (rl < 63) ? rl : 63;
   return (n - fl_cs(k) + rlast) / 16 + 1;
 }
 // link k-1 -> k: ring block b holds columns cs_k + 16b .. +15 of row 64k;
 // producer phase q writes block q - fl_dq(k); its last block is fl_bmax(k)
 __host__ __device__ __forceinline__ int fl_delta(int kc) { return fl_cs(kc - 1) + 1 - fl_cs(kc); }
 __host__ __device__ __forceinline__ int fl_dq(int kc) { return 4 - fl_delta(kc) / 16; }
-__host__ __device__ __forceinline__ int fl_bmax(int kc, int m, int n) { return fl_P(kc - 1, m, n) - 1 - fl_dq(kc); }
+__host__ __device__ __forceinline__ int fl_bmax(int kc, int m, int n, int R = 1) {
+  return fl_P(kc - 1, m, n, R) - 1 - fl_dq(kc);
+}
 // bytes per LDS code copy for n columns (covers the prefetch one phase past a stripe's last)
 __host__ __device__ __forceinline__ int fl_code_bytes(int n) { return ((n + 208) + 15) & ~15; }
 
@@ -162,6 +166,13 @@ __device__ __forceinline__ void ds_handoff(unsigned long long m63, unsigned ra, 
       : "memory");
 }
 
+#ifdef FL_X_NOHAND
+__device__ __forceinline__ void ds_handoff_lite(unsigned long long m63, unsigned pa, int pv) {
+  unsigned long long sv;
+  asm volatile("s_mov_b64 %[sv], exec\n\ts_mov_b64 exec, %[m]\n\tds_write_b32 %[pa], %[pv]\n\ts_mov_b64 exec, %[sv]\n\ts_nop 4"
+               : [sv] "=&s"(sv) : [m] "s"(m63), [pa] "v"(pa), [pv] "v"(pv) : "memory");
+}
+#endif
 // Substitution profile of a row: score + g (X-space) or + 2g (G-space) for
 // codes 0..7; code 7 = virtual column (outside [1, n]): score 0 without the
 // floor (keeps H = 0 left of column 1, never above a real cell right of n),
@@ -210,12 +221,13 @@ struct FillArgs {
   int m, n, pmax, nseg, brw, match, mismatch, g;
   unsigned ep;
 };
-template <bool FLOOR, bool TRACKPOS>
+template <bool FLOOR, bool TRACKPOS, int R>
 __device__ __attribute__((noinline)) void fill_block(const FillArgs f, int blk, int lane, int* lds);
 
-template <bool FLOOR, bool BEST, bool SAVE, bool TRACKPOS>
+template <bool FLOOR, bool BEST, bool SAVE, bool TRACKPOS, int R = 1>
 __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
   constexpr bool GS = !FLOOR;
+  static_assert(R == 1 || (R == 2 && !BEST), "two rows per lane: pass-2 plans only");
   extern __shared__ __attribute__((aligned(16))) int smem[];
   const msa_kparams& kp = a.kp;
   const int lane = threadIdx.x & 63;
@@ -230,7 +242,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
   const int L8 = kp.lds_code_bytes;
   const msa_pair_desc pd = a.pairs[0];
   const int m = pd.m, n = pd.n;
-  const int S = (m + 63) / 64;
+  const int S = (m + 64 * R - 1) / (64 * R);
   const int g = kp.gap_ext;
   const unsigned ep = kp.epoch;
   const int grp = (int)(blockIdx.x & 7), chunk = kp.sched_cap;
@@ -251,7 +263,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         const FillArgs f{a.A, a.cod, a.br, a.snap, a.outH, a.blk, a.err, a.cod_copy, a.pairs[0].a_off,
                          a.pairs[0].cod_off, a.pairs[0].out_off, a.pairs[0].m, a.pairs[0].n, a.pairs[0].pmax,
                          a.nseg, a.brw, kp.match, kp.mismatch, kp.gap_ext, kp.epoch};
-        fill_block<FLOOR, TRACKPOS>(f, a.border[t], lane, smem + w * 544);
+        fill_block<FLOOR, TRACKPOS, R>(f, a.border[t], lane, smem + w * 544);
       }
       return;
     }
@@ -286,8 +298,8 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
       int* pub = flags + 32;
       const int* cons = flags + 33;  // compute wave 0's finished phases = blocks it no longer needs
       const int cs_c = fl_cs(k0);
-      const int Pc = fl_P(k0, m, n);
-      const int Bmax = (k0 == 0) ? Pc - 1 : min(Pc - 1, fl_bmax(k0, m, n));
+      const int Pc = fl_P(k0, m, n, R);
+      const int Bmax = (k0 == 0) ? Pc - 1 : min(Pc - 1, fl_bmax(k0, m, n, R));
       const uint8_t* gcod = a.cod + pd.cod_off;
       int Yr = 0;  // bytes [0, Yr) of every LDS code copy are loaded
       auto load_codes = [&](int Y1) __attribute__((always_inline)) {
@@ -379,7 +391,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
 #pragma unroll
       for (int l = 0; l <= W; ++l) {
         bl[l] = 0;
-        bmx[l] = (l >= 1 && k0 + l < S && (SAVE || l == W)) ? fl_bmax(k0 + l, m, n) : -1;
+        bmx[l] = (l >= 1 && k0 + l < S && (SAVE || l == W)) ? fl_bmax(k0 + l, m, n, R) : -1;
       }
       unsigned long long* g_out = a.gbuf + (size_t)item * a.gbuf_stride;
       unsigned spins = 0;
@@ -420,11 +432,12 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
       // =================== compute wave: stripe k ===================
       const int k = k0 + w;
       const int cs = fl_cs(k);
-      const int P = fl_P(k, m, n);
-      const int row_i = 64 * k + lane + 1;
+      const int P = fl_P(k, m, n, R);
+      const int row_i = 64 * R * k + R * lane + 1;  // (R = 2: rows row_i, row_i + 1)
       const unsigned ac = (row_i <= m) ? (a.A[pd.a_off + row_i - 1] & 7u) : 0u;
+      const unsigned ac2 = (R == 2 && row_i + 1 <= m) ? (a.A[pd.a_off + row_i] & 7u) : 0u;
       const bool has_out = (k < S - 1);
-      const int Bin = (k == 0) ? P - 1 : min(P - 1, fl_bmax(k, m, n));
+      const int Bin = (k == 0) ? P - 1 : min(P - 1, fl_bmax(k, m, n, R));
       const int dq_in = (w == 0) ? 0 : fl_dq(k);  // producer's counter counts phases (io-in: blocks)
       const int dq = has_out ? fl_dq(k + 1) : 0;  // phase q writes out block q - dq
       // LDS byte addresses (32-bit, for the inline-asm DS ops)
@@ -437,8 +450,9 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
       const unsigned a_cons2 = lds_addr(flags + 64 + w + 1);
       const bool two_cons = SAVE || (w + 1 == W);
       const unsigned a_dummy = lds_addr(flags + 96 + 8 * (w & 1));  // sink for a phase with nothing to hand off
-      unsigned plo, phi;
+      unsigned plo, phi, plo2 = 0, phi2 = 0;
       fl_profile<GS, FLOOR>(kp.match, kp.mismatch, g, ac, plo, phi);
+      if constexpr (R == 2) fl_profile<GS, FLOOR>(kp.match, kp.mismatch, g, ac2, plo2, phi2);
       // LDS code address: column cs - lane + t, copy x = (cs - lane + OFF) & 7
       unsigned a_code;
       {
@@ -455,8 +469,12 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         if constexpr (BEST) asm("" : "+v"(gk[kx]));  // VGPR constants: H = v_add3(G, -ct_q, -g k)
       }
 
-      int X = GS ? g * (64 * k + cs) : -g;      // left neighbour at step 0 (virtual cell, H = 0)
-      int U = GS ? g * (64 * k + cs - 1) : -g;  // diagonal at step 0
+      // left neighbour and diagonal at step 0 (virtual cells, H = 0); R = 2: X/U row
+      // row_i, X2 row row_i + 1 (its diagonal is row row_i's left neighbour, its up
+      // row row_i's new value: no state of its own)
+      int X = GS ? g * (64 * R * k + (R - 1) * lane + cs) : -g;
+      int U = GS ? g * (64 * R * k + (R - 1) * lane + cs - 1) : -g;
+      int X2 = GS ? X + g : -g;
       int best = 0;
       int pubv = 0, consv = 0;
       unsigned spins = 0;
@@ -536,9 +554,10 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         }
         if constexpr (SAVE) {
           if (q % FL_PS == 0) {  // pass 2 restarts here: each lane's left and diagonal values
-            unsigned long long* sp = a.snap + ((size_t)k * a.nseg + q / FL_PS) * 128 + lane;
+            unsigned long long* sp = a.snap + ((size_t)k * a.nseg + q / FL_PS) * (128 * R) + lane;
             gstore(sp, ((unsigned long long)ep << 32) | (unsigned)X);
             gstore(sp + 64, ((unsigned long long)ep << 32) | (unsigned)U);
+            if constexpr (R == 2) gstore(sp + 128, ((unsigned long long)ep << 32) | (unsigned)X2);
           }
         }
         int hv[16], xo[16];
@@ -547,14 +566,33 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const unsigned s4 = __builtin_amdgcn_perm(phi, plo, CW[u]);
+          const unsigned s4b = (R == 2) ? __builtin_amdgcn_perm(phi2, plo2, CW[u]) : 0u;
 #pragma unroll
           for (int kk = 0; kk < 4; ++kk) {
             const int kx = 4 * u + kk;
             if (kx == FL_PF) issue_reads(q + 1, INn, CWn, pubn);  // prefetch phase q+1 (6 DS ops)
             const int s = ((int)(s4 << (24 - 8 * kk))) >> 24;
-            const int h = fl_step<GS, FLOOR>(IN[kx >> 2][kx & 3], s, X, U, g);
-            xo[kx] = X;
-            if constexpr (BEST) hv[kx] = GS ? h + negct + gk[kx] : h;
+            if constexpr (R == 1) {
+              const int h = fl_step<GS, FLOOR>(IN[kx >> 2][kx & 3], s, X, U, g);
+              xo[kx] = X;
+              if constexpr (BEST) hv[kx] = GS ? h + negct + gk[kx] : h;
+            } else {
+              // row 1's up = the previous lane's row 2 (lane 0: the producer's value);
+              // row 2's up = row 1's new value, its diagonal = row 1's previous value
+              const int sb = ((int)(s4b << (24 - 8 * kk))) >> 24;
+              const int up = dpp_shr1(IN[kx >> 2][kx & 3], X2);
+              int h1 = imax3(U + s, up, X);
+              if constexpr (FLOOR) h1 = imax(h1, 0);
+              asm("" : "+v"(h1));
+              U = up;
+              const int xprev = X;
+              X = GS ? h1 : h1 - g;
+              int h2 = imax3(xprev + sb, X, X2);
+              if constexpr (FLOOR) h2 = imax(h2, 0);
+              asm("" : "+v"(h2));
+              X2 = GS ? h2 : h2 - g;
+              xo[kx] = X2;
+            }
           }
         }
         if constexpr (BEST) {
@@ -568,8 +606,13 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         const bool wr = has_out && bq >= 0;
         if (wr && consv < bq - (FL_RINGB - 1)) refresh_cons(bq - (FL_RINGB - 1));
         const unsigned wa = wr ? a_ring_out + (unsigned)((bq & (FL_RINGB - 1)) * 64) : a_dummy;
+#ifndef FL_X_NOHAND
         ds_handoff(m63, wa, fl_v4i{xo[0], xo[1], xo[2], xo[3]}, fl_v4i{xo[4], xo[5], xo[6], xo[7]},
                    fl_v4i{xo[8], xo[9], xo[10], xo[11]}, fl_v4i{xo[12], xo[13], xo[14], xo[15]}, a_prog_me, q + 1);
+#else
+        asm volatile("" :: "v"(xo[0]), "v"(xo[5]), "v"(xo[10]), "v"(xo[15]));
+        ds_handoff_lite(m63, a_prog_me, q + 1);
+#endif
 #ifdef MSA_STAMPS
         if (q == dq) FL_STAMP(0, 3, __builtin_amdgcn_s_memrealtime());
 #endif
@@ -636,33 +679,37 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
 // Pass 2: block (stripe s, segment seg) of FL_PS phases, one wave.  Its inputs
 // are {epoch, value} granules that pass 1 may still be writing: the wave waits
 // for the block's last bottom-row granule, then loads and checks them all.
-template <bool FLOOR, bool TRACKPOS>
+// R = 2: lane r holds rows 128s+2r+1 (X/U) and 128s+2r+2 (X2/U2); cells go to the
+// R = 2 layout (per 4 steps a lane writes its two rows' int4s side by side).
+template <bool FLOOR, bool TRACKPOS, int R>
 __device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, int lane, int* lds) {
   constexpr bool GS = !FLOOR;
   const unsigned ep = a.ep;
-  const int m = a.m, n = a.n, S = (m + 63) / 64, g = a.g;
+  const int m = a.m, n = a.n, S = (m + 64 * R - 1) / (64 * R), g = a.g;
   const int s = blk / a.nseg, seg = blk - s * a.nseg;
   int bb = INT32_MIN, bi = 0, bj = 0;
 #if defined(FL_EXP) && FL_EXP == 1
   return;
 #endif
   if (s < S) {
-    const int P = fl_P(s, m, n);
+    const int P = fl_P(s, m, n, R);
     const int q0 = seg * FL_PS;
     if (q0 < P) {
       int q1 = min(P, q0 + FL_PS);
       const int cs = fl_cs(s);
-      const int row_i = 64 * s + lane + 1;
+      const int row_i = 64 * R * s + R * lane + 1;
       const unsigned ac = (row_i <= m) ? (a.A[a.a_off + row_i - 1] & 7u) : 0u;
-      unsigned plo, phi;
+      const unsigned ac2 = (R == 2 && row_i + 1 <= m) ? (a.A[a.a_off + row_i] & 7u) : 0u;
+      unsigned plo, phi, plo2 = 0, phi2 = 0;
       fl_profile<GS, FLOOR>(a.match, a.mismatch, g, ac, plo, phi);
-      const int Bin = (s == 0) ? P - 1 : min(P - 1, fl_bmax(s, m, n));
-      const unsigned long long* sp = a.snap + ((size_t)s * a.nseg + seg) * 128 + lane;
+      if constexpr (R == 2) fl_profile<GS, FLOOR>(a.match, a.mismatch, g, ac2, plo2, phi2);
+      const int Bin = (s == 0) ? P - 1 : min(P - 1, fl_bmax(s, m, n, R));
+      const unsigned long long* sp = a.snap + ((size_t)s * a.nseg + seg) * (128 * R) + lane;
       const unsigned long long* brow = a.br + (size_t)(s > 0 ? s - 1 : 0) * a.brw;
       // bottom-row blocks [q0, qb) of the row above come from pass 1 (s > 0)
       const int qb = (s > 0) ? min(q1, Bin + 1) : q0;
       const int nv = 16 * max(0, qb - q0);  // granules, lane l holds l, l+64, ...
-      int X = 0, U = 0;
+      int X = 0, U = 0, X2 = 0;
       // uniform waits (ballots) and no early exits: the compiler keeps the wave whole
       bool ready = (nv == 0);
       for (int t2 = 0; !ready && t2 < (int)(FL_SPIN_MAX >> 2); ++t2) {  // the block's last granule first
@@ -677,6 +724,11 @@ __device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, 
           bool ok = ((unsigned)(x0 >> 32) == ep) && ((unsigned)(u0 >> 32) == ep);
           X = (int)(unsigned)x0;
           U = (int)(unsigned)u0;
+          if constexpr (R == 2) {
+            const unsigned long long x2 = gload(sp + 128);
+            ok = ok && ((unsigned)(x2 >> 32) == ep);
+            X2 = (int)(unsigned)x2;
+          }
           for (int v = lane; v < nv; v += 64) {
             const unsigned long long gv = gload(brow + 16 * q0 + v);
             ok = ok && ((unsigned)(gv >> 32) == ep);
@@ -700,15 +752,16 @@ __device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, 
       const int b0 = cs - lane - 1 + MSA_CPAD;
       const unsigned* cptr = reinterpret_cast<const unsigned*>(a.cod + (size_t)(b0 & (MSA_NCOPY - 1)) * a.cod_copy +
                                                              a.cod_off + (b0 & ~(MSA_NCOPY - 1)));
-      const int negct0 = -g * (64 * s + 1 + cs);
+      // H = G - g(i+j); i+j = 64Rs + 1 + cs + t + (R-1) lane on row 1, +1 on row 2
+      const int negct0 = -g * (64 * R * s + 1 + cs + (R - 1) * lane);
       int gk[16];
 #pragma unroll
       for (int kx = 0; kx < 16; ++kx) {
         gk[kx] = -g * kx;
         asm("" : "+v"(gk[kx]));
       }
-      int best = INT32_MIN, bt = -1;
-      msa_v4i* hp = reinterpret_cast<msa_v4i*>(a.outH + (size_t)a.out_off + (size_t)s * a.pmax * MSA_K * 64) + lane;
+      int best = INT32_MIN, bt = -1, best2 = INT32_MIN, bt2 = -1;
+      msa_v4i* hp = reinterpret_cast<msa_v4i*>(a.outH + (size_t)a.out_off + (size_t)s * a.pmax * MSA_K * 64 * R) + R * lane;
       for (int q = q0; q < q1; ++q) {
         int IN[16];
         if (q <= Bin) {
@@ -730,31 +783,62 @@ __device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, 
         const uint4 c4 = *reinterpret_cast<const uint4*>(cptr + 4 * q);
         const unsigned cw[4] = {c4.x, c4.y, c4.z, c4.w};
         const int negct = negct0 - 16 * g * q;
-        int hv[16];
+        int hv[16], hv2[16];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const unsigned s4 = __builtin_amdgcn_perm(phi, plo, cw[u]);
+          const unsigned s4b = (R == 2) ? __builtin_amdgcn_perm(phi2, plo2, cw[u]) : 0u;
 #pragma unroll
           for (int kk = 0; kk < 4; ++kk) {
             const int kx = 4 * u + kk;
             const int sc = ((int)(s4 << (24 - 8 * kk))) >> 24;
-            const int h = fl_step<GS, FLOOR>(IN[kx], sc, X, U, g);
-            hv[kx] = GS ? h + negct + gk[kx] : h;
+            if constexpr (R == 1) {
+              const int h = fl_step<GS, FLOOR>(IN[kx], sc, X, U, g);
+              hv[kx] = GS ? h + negct + gk[kx] : h;
+            } else {
+              const int sb = ((int)(s4b << (24 - 8 * kk))) >> 24;
+              const int up = dpp_shr1(IN[kx], X2);
+              int h1 = imax3(U + sc, up, X);
+              if constexpr (FLOOR) h1 = imax(h1, 0);
+              asm("" : "+v"(h1));
+              U = up;
+              const int xprev = X;
+              X = GS ? h1 : h1 - g;
+              int h2 = imax3(xprev + sb, X, X2);
+              if constexpr (FLOOR) h2 = imax(h2, 0);
+              asm("" : "+v"(h2));
+              X2 = GS ? h2 : h2 - g;
+              hv[kx] = GS ? h1 + negct + gk[kx] : h1;
+              hv2[kx] = GS ? h2 + negct + gk[kx] - g : h2;
+            }
             if constexpr (TRACKPOS) {
               if (hv[kx] > best) { best = hv[kx]; bt = 16 * q + kx; }
+              if (R == 2 && hv2[kx] > best2) { best2 = hv2[kx]; bt2 = 16 * q + kx; }
             }
           }
           __builtin_nontemporal_store(msa_v4i{hv[4 * u], hv[4 * u + 1], hv[4 * u + 2], hv[4 * u + 3]},
-                                      hp + (size_t)(4 * q + u) * 64);
+                                      hp + (size_t)(4 * q + u) * 64 * R);
+          if constexpr (R == 2)
+            __builtin_nontemporal_store(msa_v4i{hv2[4 * u], hv2[4 * u + 1], hv2[4 * u + 2], hv2[4 * u + 3]},
+                                        hp + (size_t)(4 * q + u) * 128 + 1);
         }
         if constexpr (!TRACKPOS) {
 #pragma unroll
           for (int kx = 0; kx < 16; kx += 2) best = imax3(best, hv[kx], hv[kx + 1]);
+          if constexpr (R == 2) {
+#pragma unroll
+            for (int kx = 0; kx < 16; kx += 2) best2 = imax3(best2, hv2[kx], hv2[kx + 1]);
+          }
         }
       }
       bb = (row_i <= m) ? best : INT32_MIN;
       bi = row_i;
       bj = TRACKPOS ? cs + bt - lane : -1;
+      if (R == 2 && row_i + 1 <= m && best2 > bb) {  // ties keep the upper row
+        bb = best2;
+        bi = row_i + 1;
+        bj = TRACKPOS ? cs + bt2 - lane : -1;
+      }
     }
   }
   // first max in row-major order: max score, then min row, then min column

@@ -41,6 +41,7 @@ class PairGeom:
     stripe0: int
     pmax: int
     out_off: int
+    rows_per_lane: int = 1  # 2: 128-row stripes, lane r holds rows 2r+1, 2r+2 (two-pass flow plans)
 
 
 class Plan:
@@ -74,8 +75,8 @@ class Plan:
         lay = (C.c_int64 * 4)()
         for k, (m, n) in enumerate(zip(self.ms, self.ns)):
             LB.check(L.msa_plan_pair_layout(self._h, k, lay), "msa_plan_pair_layout")
-            self.geom.append(PairGeom(m, n, int(lay[0]), int(lay[1]), int(lay[2])))
-        self.phase_steps = int(lay[3])
+            self.geom.append(PairGeom(m, n, int(lay[0]), int(lay[1]), int(lay[2]), max(1, int(lay[3]) >> 16)))
+        self.phase_steps = int(lay[3]) & 0xFFFF
 
     def __del__(self):
         try:
@@ -116,20 +117,22 @@ class Plan:
     def deskew(self, flat: np.ndarray, pair: int, meta: np.ndarray, fill=0) -> np.ndarray:
         """Row-major (m+1) x (n+1) matrix of a pair's int32 cells (row/col 0 = fill)."""
         g = self.geom[pair]
-        S = (g.m + 63) // 64
-        blk = flat[g.out_off:g.out_off + S * g.pmax * 1024].reshape(S, g.pmax * 4, 64, 4)
+        R = g.rows_per_lane
+        S = (g.m + 64 * R - 1) // (64 * R)
+        blk = flat[g.out_off:g.out_off + S * g.pmax * 1024 * R].reshape(S, g.pmax * 4, 64, R, 4)
         out = np.full((g.m + 1, g.n + 1), fill, dtype=flat.dtype)
         T = g.pmax * 16
         t = np.arange(T)
         r = np.arange(64)
         for s in range(S):
             cs = int(meta[g.stripe0 + s, 0])
-            vals = blk[s].transpose(1, 0, 2).reshape(64, T)  # [r][t]
-            i = 64 * s + r + 1
             j = cs + t[None, :] - r[:, None]
-            ok = (i[:, None] <= g.m) & (j >= 0) & (j <= g.n)
-            ii = np.broadcast_to(i[:, None], j.shape)
-            out[ii[ok], j[ok]] = vals[ok]
+            for rho in range(R):
+                vals = blk[s, :, :, rho, :].transpose(1, 0, 2).reshape(64, T)  # [r][t]
+                i = 64 * R * s + R * r + rho + 1
+                ok = (i[:, None] <= g.m) & (j >= 0) & (j <= g.n)
+                ii = np.broadcast_to(i[:, None], j.shape)
+                out[ii[ok], j[ok]] = vals[ok]
         return out
 
     def deskew_dir(self, flat: np.ndarray, pair: int, meta: np.ndarray) -> np.ndarray:

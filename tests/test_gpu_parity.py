@@ -106,13 +106,15 @@ def test_sw_linear_single_score_only(oracle, dev, LB, scoring, track_end):
             assert tuple(res["end"]) == tuple(o["end"]), (m, n)
 
 
-@pytest.mark.parametrize("flow", ["0", "1"])
-def test_sw_linear_single_flow_switch(oracle, dev, LB, monkeypatch, flow):
-    """MSA_FLOW=0 keeps the one-pass stripe kernel for single pairs; both give the oracle's H."""
+@pytest.mark.parametrize("flow,rows", [("0", "1"), ("1", "1"), ("1", "2")])
+def test_sw_linear_single_flow_switch(oracle, dev, LB, monkeypatch, flow, rows):
+    """MSA_FLOW=0 keeps the one-pass stripe kernel for single pairs; the two-pass flow plans
+    run one (MSA_R=1) or two (MSA_R=2, default) rows per lane; all give the oracle's H."""
     import torch
     from cse305_parallel_sequence_alignment_amd.plan import Plan
 
     monkeypatch.setenv("MSA_FLOW", flow)
+    monkeypatch.setenv("MSA_R", rows)
     rng = np.random.default_rng(29)
     for (ma, mi, g), (m, n) in [((1, 0, 1), (2100, 1900)), ((2, -1, 1), (1800, 2300))]:
         A, B = rs(rng, m), rs(rng, n)
@@ -122,8 +124,10 @@ def test_sw_linear_single_flow_switch(oracle, dev, LB, monkeypatch, flow):
         pl.run(_dev(A, dev), _dev(B, dev), H)
         res = pl.results()[0]
         o = oracle.sw(A, B, ma, mi, g, g, want_h=True)
+        assert pl.geom[0].rows_per_lane == (int(rows) if flow == "1" else 1)
         assert (res["score"], tuple(res["end"])) == (o["score"], tuple(o["end"])), (m, n)
         assert pl.checksum(H) == oracle.checksum_h(o["H"])
+        assert np.array_equal(pl.deskew(H.cpu().numpy(), 0, pl.stripe_meta())[1:, 1:], o["H"][1:, 1:])
 
 
 @pytest.mark.parametrize("scoring", [(2, -1, 1), (1, 0, 1)])
