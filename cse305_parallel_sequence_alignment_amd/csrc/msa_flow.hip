@@ -679,8 +679,8 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
 // Pass 2: block (stripe s, segment seg) of FL_PS phases, one wave.  Its inputs
 // are {epoch, value} granules that pass 1 may still be writing: the wave waits
 // for the block's last bottom-row granule, then loads and checks them all.
-// R = 2: lane r holds rows 128s+2r+1 (X/U) and 128s+2r+2 (X2/U2); cells go to the
-// R = 2 layout (per 4 steps a lane writes its two rows' int4s side by side).
+// R = 2: lane r holds rows 128s+2r+1 (X/U) and 128s+2r+2 (X2); cells go to the
+// R = 2 layout (per 4 steps: the wave's row-1 int4s, then its row-2 int4s).
 template <bool FLOOR, bool TRACKPOS, int R>
 __device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, int lane, int* lds) {
   constexpr bool GS = !FLOOR;
@@ -761,7 +761,7 @@ __device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, 
         asm("" : "+v"(gk[kx]));
       }
       int best = INT32_MIN, bt = -1, best2 = INT32_MIN, bt2 = -1;
-      msa_v4i* hp = reinterpret_cast<msa_v4i*>(a.outH + (size_t)a.out_off + (size_t)s * a.pmax * MSA_K * 64 * R) + R * lane;
+      msa_v4i* hp = reinterpret_cast<msa_v4i*>(a.outH + (size_t)a.out_off + (size_t)s * a.pmax * MSA_K * 64 * R) + lane;
       for (int q = q0; q < q1; ++q) {
         int IN[16];
         if (q <= Bin) {
@@ -818,9 +818,9 @@ __device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, 
           }
           __builtin_nontemporal_store(msa_v4i{hv[4 * u], hv[4 * u + 1], hv[4 * u + 2], hv[4 * u + 3]},
                                       hp + (size_t)(4 * q + u) * 64 * R);
-          if constexpr (R == 2)
+          if constexpr (R == 2)  // (each store: one contiguous 1 KiB)
             __builtin_nontemporal_store(msa_v4i{hv2[4 * u], hv2[4 * u + 1], hv2[4 * u + 2], hv2[4 * u + 3]},
-                                        hp + (size_t)(4 * q + u) * 128 + 1);
+                                        hp + (size_t)(4 * q + u) * 128 + 64);
         }
         if constexpr (!TRACKPOS) {
 #pragma unroll

@@ -1241,21 +1241,20 @@ __device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
 }
 
 // R rows per lane (two-pass flow plans may use R = 2): element
-// ((s*pmax*4 + t/4)*64 + r)*4R + rho*4 + t%4 <-> cell (64Rs + Rr + rho + 1, cs_s + t - r)
+// ((s*pmax*4 + t/4)*R + rho)*256 + r*4 + t%4 <-> cell (64Rs + Rr + rho + 1, cs_s + t - r)
 __global__ void checksum_kernel(const int32_t* H, const msa_pair_desc* pairs, const msa_stripe_meta* meta, int pair,
                                 int band, int R, unsigned long long* out) {
   const msa_pair_desc pd = pairs[pair];
   const int S = (pd.m + 64 * R - 1) / (64 * R);
   const long long per_stripe = (long long)pd.pmax * MSA_K * 64 * R;
   const long long total = per_stripe * S;
-  const int sh = (R == 2) ? 3 : 2;
   unsigned long long acc = 0;
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
     const int s = (int)(e / per_stripe);
     const long long rem = e - (long long)s * per_stripe;
-    const int quad = (int)(rem >> (6 + sh));  // /(64*4R)
-    const int r = (int)((rem >> sh) & 63);
-    const int rho = (R == 2) ? (int)((rem >> 2) & 1) : 0;
+    const int quad = (int)((rem >> 8) / R);  // /(256R)
+    const int rho = (int)((rem >> 8) - (long long)quad * R);
+    const int r = (int)((rem >> 2) & 63);
     const int t = quad * 4 + (int)(rem & 3);
     const int i = 64 * R * s + R * r + rho + 1;
     const int j = meta[pd.stripe0 + s].cs + t - r;

@@ -119,7 +119,7 @@ class Plan:
         g = self.geom[pair]
         R = g.rows_per_lane
         S = (g.m + 64 * R - 1) // (64 * R)
-        blk = flat[g.out_off:g.out_off + S * g.pmax * 1024 * R].reshape(S, g.pmax * 4, 64, R, 4)
+        blk = flat[g.out_off:g.out_off + S * g.pmax * 1024 * R].reshape(S, g.pmax * 4, R, 64, 4)
         out = np.full((g.m + 1, g.n + 1), fill, dtype=flat.dtype)
         T = g.pmax * 16
         t = np.arange(T)
@@ -128,7 +128,7 @@ class Plan:
             cs = int(meta[g.stripe0 + s, 0])
             j = cs + t[None, :] - r[:, None]
             for rho in range(R):
-                vals = blk[s, :, :, rho, :].transpose(1, 0, 2).reshape(64, T)  # [r][t]
+                vals = blk[s, :, rho, :, :].transpose(1, 0, 2).reshape(64, T)  # [r][t]
                 i = 64 * R * s + R * r + rho + 1
                 ok = (i[:, None] <= g.m) & (j >= 0) & (j <= g.n)
                 ii = np.broadcast_to(i[:, None], j.shape)

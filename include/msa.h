@@ -156,7 +156,7 @@ int64_t msa_plan_stripes(const msa_plan* plan);
  * pair's block, DP steps per kernel phase | R << 16}.  R = rows per lane
  * (0 means 1).  Cell (i, j) of stripe s = (i-1)/(64R), lane r = ((i-1)%(64R))/R,
  * row rho = (i-1)%R, step t = j - cs_s + r lives at element
- * out_off + ((s*pmax*4 + t/4)*64 + r)*4R + rho*4 + t%4 (DIR bytes, R = 1:
+ * out_off + ((s*pmax*4 + t/4)*R + rho)*256 + r*4 + t%4 (DIR bytes, R = 1:
  * (s*pmax + t/16)*1024 + r*16 + t%16), cs_s = meta[12*(stripe0+s)].  R = 2 only
  * for two-pass single-pair SW-linear H plans (MSA_R=2). */
 int msa_plan_pair_layout(const msa_plan* plan, int64_t pair, int64_t* out4);
