@@ -531,11 +531,10 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
   a.brw = P->brw;
   a.nseg = P->nseg;
   a.nblk = env_int("MSA_NOFILL", 0) ? 0 : P->nblk;  // (diagnostic: pass 1 alone)
-  HIPCHK(hipMemsetAsync(P->d_ticket, 0, 64, st));
   {
     const unsigned virt = (P->kp.alg == MSA_ALG_SWL || P->kp.alg == MSA_ALG_SWL0 || P->kp.alg == MSA_ALG_SWA) ? MSA_VIRT_CODE : 0u;
     hipLaunchKernelGGL(stage_codes_kernel, dim3(64, (unsigned)P->segs.size()), dim3(256), 0, st, dB, P->d_segs,
-                       (int)P->segs.size(), P->d_cod, (long long)P->cod_copy, virt);
+                       (int)P->segs.size(), P->d_cod, (long long)P->cod_copy, virt, P->d_ticket);
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipEventRecord(P->ev0, st));

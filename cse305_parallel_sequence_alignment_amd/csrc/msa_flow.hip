@@ -850,21 +850,28 @@ __device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, 
   if (lane == 0) a.blk[blk] = make_int4(bb, bi, bj, 0);
 }
 
-// Pair result of a two-pass plan from the pass-2 block bests.
+// Pair result of a two-pass plan from the pass-2 block bests: every thread folds
+// a strided share (loads all in flight), then wave shuffles, then 4 wave results.
 __global__ __launch_bounds__(256) void reduce_blocks_kernel(const int4* blk, int nblk, PairResult* out) {
-  __shared__ int4 sh[256];
-  int b = 0, bi = 0, bj = 0;  // empty alignment: score 0 at (0, 0)
+  __shared__ int4 sh[4];
+  // empty alignment: score 0 at (0, 0); first maximum in row-major order
   auto better = [](int vb, int vi, int vj, int b_, int i_, int j_) {
     return vb > b_ || (vb == b_ && vb > 0 && (vi < i_ || (vi == i_ && vj < j_)));
   };
+  int b = 0, bi = 0, bj = 0;
   for (int x = threadIdx.x; x < nblk; x += 256) {
     const int4 v = blk[x];
     if (better(v.x, v.y, v.z, b, bi, bj)) { b = v.x; bi = v.y; bj = v.z; }
   }
-  sh[threadIdx.x] = make_int4(b, bi, bj, 0);
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const int ob = __shfl_xor(b, off), oi = __shfl_xor(bi, off), oj = __shfl_xor(bj, off);
+    if (better(ob, oi, oj, b, bi, bj)) { b = ob; bi = oi; bj = oj; }
+  }
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = make_int4(b, bi, bj, 0);
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int x = 1; x < 256; ++x) {
+    for (int x = 1; x < 4; ++x) {
       const int4 v = sh[x];
       if (better(v.x, v.y, v.z, b, bi, bj)) { b = v.x; bi = v.y; bj = v.z; }
     }

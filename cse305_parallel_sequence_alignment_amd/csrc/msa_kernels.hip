@@ -1159,7 +1159,9 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
 // copy c, byte x of pair p = code of column x + c - CPAD + 1 (virt outside [1, n]).
 // ---------------------------------------------------------------------------
 __global__ void stage_codes_kernel(const uint8_t* B, const msa_pair_desc* pairs, int n_pairs, uint8_t* cod,
-                                   long long cod_copy, unsigned virt) {
+                                   long long cod_copy, unsigned virt, int* ticket) {
+  // the run's ticket counters and error word start at 0 (this launch precedes the DP kernel)
+  if (ticket && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 16) ticket[threadIdx.x] = 0;
   const int p = blockIdx.y;
   if (p >= n_pairs) return;
   const msa_pair_desc pd = pairs[p];
