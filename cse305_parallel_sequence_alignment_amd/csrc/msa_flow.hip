@@ -54,6 +54,9 @@ namespace msa {
 #ifndef FL_PF
 #define FL_PF 8         // step of a phase at which the next phase's inputs are read
 #endif
+#ifndef FL_FSLEEP
+#define FL_FSLEEP 32    // s_sleep between a pass-2 wave's polls of its block's last granule
+#endif
 #ifndef FL_IOSLEEP
 #define FL_IOSLEEP 1    // s_sleep of an idle io wave
 #endif
@@ -715,7 +718,7 @@ __device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, 
       for (int t2 = 0; !ready && t2 < (int)(FL_SPIN_MAX >> 2); ++t2) {  // the block's last granule first
         const unsigned long long gl = gload(brow + 16 * q0 + nv - 1);
         ready = __ballot((unsigned)(gl >> 32) != ep) == 0;
-        if (!ready) __builtin_amdgcn_s_sleep(32);
+        if (!ready) __builtin_amdgcn_s_sleep(FL_FSLEEP);
       }
       if (ready) {
         ready = false;
@@ -762,7 +765,17 @@ __device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, 
       }
       int best = INT32_MIN, bt = -1, best2 = INT32_MIN, bt2 = -1;
       msa_v4i* hp = reinterpret_cast<msa_v4i*>(a.outH + (size_t)a.out_off + (size_t)s * a.pmax * MSA_K * 64 * R) + lane;
+      // column codes 4 phases ahead (one global dwordx4 per phase; ~1 us away otherwise)
+      auto ldc = [&](int q) __attribute__((always_inline)) {
+        return *reinterpret_cast<const uint4*>(cptr + 4 * min(q, P - 1));
+      };
+      uint4 cr0 = ldc(q0), cr1 = ldc(q0 + 1), cr2 = ldc(q0 + 2), cr3 = ldc(q0 + 3);
       for (int q = q0; q < q1; ++q) {
+        const uint4 c4 = cr0;
+        cr0 = cr1;
+        cr1 = cr2;
+        cr2 = cr3;
+        cr3 = ldc(q + 4);
         int IN[16];
         if (q <= Bin) {
           if (s == 0) {
@@ -780,7 +793,6 @@ __device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, 
 #pragma unroll
           for (int j = 0; j < 16; ++j) IN[j] = MSA_NEG;
         }
-        const uint4 c4 = *reinterpret_cast<const uint4*>(cptr + 4 * q);
         const unsigned cw[4] = {c4.x, c4.y, c4.z, c4.w};
         const int negct = negct0 - 16 * g * q;
         int hv[16], hv2[16];

@@ -9,6 +9,7 @@ from oracle.oracle import load_dataset
 m = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
 n = int(sys.argv[2]) if len(sys.argv) > 2 else m
 W = int(os.environ.get("FLW", "4"))
+RR = int(os.environ.get("MSA_R", "2"))
 seqs = load_dataset()[1]
 enc = lambda s: torch.from_numpy(np.frombuffer(s.translate(bytes.maketrans(b"ACGT", b"\x00\x01\x02\x03")), dtype=np.uint8).copy()).cuda()
 A, B = (seqs[1] * 8)[:m], (seqs[0] * 8)[:n]
@@ -24,12 +25,12 @@ for it in range(4):
     pl.run(dA, dB, out)
     torch.cuda.synchronize()
     print("kernel ms", round(pl.kernel_ms(), 4), "score", pl.results()[0]["score"])
-S = (m + 63) // 64
+S = (m + 64 * RR - 1) // (64 * RR)
 items = (S + W - 1) // W
 a = st.cpu().numpy().reshape(64, 16, 4096, 4)[:items, :W, 0, :4].reshape(-1, 4)[:S].astype(np.float64)
 start, end, nslow = a[:, 0] - a[0, 0], a[:, 1] - a[0, 0], a[:, 2]
 def fl_cs(k): return -((16 - (k & 15)) & 15)
-def fl_P(k): return (n - fl_cs(k) + min(m - 64 * k - 1, 63)) // 16 + 1
+def fl_P(k): return (n - fl_cs(k) + min((m - 64 * RR * k - 1) // RR, 63)) // 16 + 1
 P = np.array([fl_P(k) for k in range(S)])
 pt = (end - start) / P * 10.0  # ns per phase (realtime = 100 MHz)
 lag = np.diff(start) * 10.0     # ns
