@@ -542,7 +542,7 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(P->ev1, st));
   if (P->flow2) {
-    hipLaunchKernelGGL(reduce_blocks_kernel, dim3(1), dim3(256), 0, st, (const int4*)P->d_blk, P->nblk, P->d_res);
+    hipLaunchKernelGGL(reduce_blocks_kernel, dim3(1), dim3(1024), 0, st, (const int4*)P->d_blk, P->nblk, P->d_res);
     HIPCHK(hipGetLastError());
     return MSA_OK;
   }

@@ -893,16 +893,20 @@ __device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, 
 
 // Pair result of a two-pass plan from the pass-2 block bests: every thread folds
 // a strided share (loads all in flight), then wave shuffles, then 4 wave results.
-__global__ __launch_bounds__(256) void reduce_blocks_kernel(const int4* blk, int nblk, PairResult* out) {
-  __shared__ int4 sh[4];
+__global__ __launch_bounds__(1024) void reduce_blocks_kernel(const int4* blk, int nblk, PairResult* out) {
+  __shared__ int4 sh[16];
   // empty alignment: score 0 at (0, 0); first maximum in row-major order
   auto better = [](int vb, int vi, int vj, int b_, int i_, int j_) {
     return vb > b_ || (vb == b_ && vb > 0 && (vi < i_ || (vi == i_ && vj < j_)));
   };
   int b = 0, bi = 0, bj = 0;
-  for (int x = threadIdx.x; x < nblk; x += 256) {
-    const int4 v = blk[x];
-    if (better(v.x, v.y, v.z, b, bi, bj)) { b = v.x; bi = v.y; bj = v.z; }
+  for (int x0 = threadIdx.x; x0 < nblk; x0 += 4096) {  // four loads in flight per thread
+    int4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = (x0 + 1024 * u < nblk) ? blk[x0 + 1024 * u] : make_int4(0, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (better(v[u].x, v[u].y, v[u].z, b, bi, bj)) { b = v[u].x; bi = v[u].y; bj = v[u].z; }
   }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
@@ -912,7 +916,7 @@ __global__ __launch_bounds__(256) void reduce_blocks_kernel(const int4* blk, int
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = make_int4(b, bi, bj, 0);
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int x = 1; x < 4; ++x) {
+    for (int x = 1; x < 16; ++x) {
       const int4 v = sh[x];
       if (better(v.x, v.y, v.z, b, bi, bj)) { b = v.x; bi = v.y; bj = v.z; }
     }
