@@ -46,7 +46,7 @@ namespace msa {
 #define FL_NCOPY 8      // byte-shifted LDS code copies (8-byte aligned 8-code reads)
 #define FL_FLAGS 128    // ints of flags at the start of LDS
 #ifndef FL_PS
-#define FL_PS 16        // phases per pass-2 segment (pass 1 saves its state every FL_PS phases)
+#define FL_PS 8         // phases per pass-2 segment (pass 1 saves its state every FL_PS phases)
 #endif
 #ifdef FL_DBG
 #define FL_SPIN_MAX (1u << 16)
