@@ -92,6 +92,7 @@ def lib() -> C.CDLL:
     L.msa_plan_pair_layout.argtypes = [P, i64, C.POINTER(i64)]
     L.msa_plan_checksum.argtypes = [P, P, i64, C.POINTER(u64), P]
     L.msa_plan_last_kernel_ms.argtypes = [P, C.POINTER(C.c_float)]
+    L.msa_plan_set_timing.argtypes = [P, i32]
     L.msa_encode_pair.argtypes = [P, sz, P, sz, P, P]
     L.msa_sw_align.argtypes = [P, sz, P, sz, i32, i32, i32, i32, C.POINTER(i32), C.POINTER(i64), C.POINTER(i64),
                                C.POINTER(i64), C.POINTER(i64), P, sz]
@@ -115,5 +116,5 @@ EXPORTED = [
     "msa_partial_partition", "msa_partial_tables", "msa_plan_create", "msa_plan_destroy", "msa_plan_cells_size",
     "msa_plan_run", "msa_plan_results", "msa_plan_stripe_meta", "msa_plan_stripes", "msa_plan_pair_layout",
     "msa_plan_checksum",
-    "msa_plan_last_kernel_ms", "msa_encode_pair", "msa_sw_align",
+    "msa_plan_last_kernel_ms", "msa_plan_set_timing", "msa_encode_pair", "msa_sw_align",
 ]

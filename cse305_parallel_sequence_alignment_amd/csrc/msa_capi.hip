@@ -151,6 +151,8 @@ struct msa_plan {
   unsigned long long* d_snap = nullptr;
   int4* d_blk = nullptr;
   int* d_order = nullptr;
+  bool timing = true;  // record HIP events around the DP kernel (msa_plan_last_kernel_ms)
+  bool timed = false;  // events of the last run exist
   int R = 1;      // flow kernel rows per lane
   int nflow = 0;  // two-pass: pass-1 workgroups (the rest of the grid runs pass-2 blocks)
   int brw = 0, nseg = 0, nblk = 0;
@@ -537,10 +539,12 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
                        (int)P->segs.size(), P->d_cod, (long long)P->cod_copy, virt, P->d_ticket);
     HIPCHK(hipGetLastError());
   }
-  HIPCHK(hipEventRecord(P->ev0, st));
+  const bool ev = P->timing;  // timing events are instrumentation: msa_plan_set_timing
+  if (ev) HIPCHK(hipEventRecord(P->ev0, st));
+  P->timed = ev;
   hipLaunchKernelGGL(P->fn, dim3(P->grid), dim3(P->threads), P->lds_bytes, st, a);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(P->ev1, st));
+  if (ev) HIPCHK(hipEventRecord(P->ev1, st));
   if (P->flow2) {
     hipLaunchKernelGGL(reduce_blocks_kernel, dim3(1), dim3(1024), 0, st, (const int4*)P->d_blk, P->nblk, P->d_res);
     HIPCHK(hipGetLastError());
@@ -558,8 +562,15 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
 extern "C" int msa_debug_stamps(msa_plan* P, unsigned long long* d) { P->stamps = d; return 0; }
 #endif
 
+int msa_plan_set_timing(msa_plan* P, int on) {
+  if (!P) return MSA_ERR_ARG;
+  P->timing = on != 0;
+  return MSA_OK;
+}
+
 int msa_plan_last_kernel_ms(msa_plan* P, float* ms) {
   if (!P || !ms) return MSA_ERR_ARG;
+  if (!P->timed) return MSA_ERR_ARG;  // no run with timing on yet
   HIPCHK(hipEventSynchronize(P->ev1));
   HIPCHK(hipEventElapsedTime(ms, P->ev0, P->ev1));
   return MSA_OK;

@@ -108,6 +108,10 @@ class Plan:
                  "msa_plan_checksum")
         return int(v.value)
 
+    def set_timing(self, on: bool) -> None:
+        """Record HIP events around the DP kernel in run() (default on; kernel_ms() needs it)."""
+        LB.check(LB.lib().msa_plan_set_timing(self._h, int(bool(on))), "msa_plan_set_timing")
+
     def kernel_ms(self) -> float:
         v = C.c_float()
         LB.check(LB.lib().msa_plan_last_kernel_ms(self._h, C.byref(v)), "msa_plan_last_kernel_ms")

@@ -163,8 +163,12 @@ int msa_plan_pair_layout(const msa_plan* plan, int64_t pair, int64_t* out4);
 /* Order-independent digest of pair `pair`'s H cells (oracle orc_checksum_h). */
 int msa_plan_checksum(msa_plan* plan, const int32_t* dH, int64_t pair, uint64_t* digest, void* stream);
 /* Device time (ms) of the last msa_plan_run's stripe kernel, from HIP events
- * recorded on the run's stream (synchronizes). */
+ * recorded on the run's stream (synchronizes).  MSA_ERR_ARG if that run had
+ * timing off. */
 int msa_plan_last_kernel_ms(msa_plan* plan, float* ms);
+/* Record the timing events in msa_plan_run (default on); off saves two stream
+ * commands per run. */
+int msa_plan_set_timing(msa_plan* plan, int on);
 
 /* Map the symbols of a pair to codes 0..7 (equality preserved, first-seen
  * order).  Returns MSA_ERR_ALPHABET for more than 8 distinct symbols. */
