@@ -8,17 +8,23 @@ launched by torch.distributed.run).  A "step" is one pass of the DP fill over
 one batch of input already resident in HBM:
 
 * c2 (default, the BASELINE metric's config): every rank aligns its own
-  10,000 x 10,000 pair (rank r: query seq(r+1)[:10000] vs the reference
-  seq0[:10000] that rank 0 broadcasts once with RCCL), Smith-Waterman, linear
-  gap, int32 scores, the full int32 H matrix written to HBM; the step ends
-  with an RCCL all-gather of the per-rank scores.  Weak scaling.
-* c4: 1024 pairs of 4,000 x 4,000 SW (score only), sharded over ranks.
-* c3: one 100k x 100k banded (|i-j| <= 512) reference-Gotoh fill, H written.
+  10,000 x 10,000 pair (rank r: query seq(r+1)[:10000] against the reference
+  seq0[:10000], which rank 0 broadcasts once with RCCL), Smith-Waterman, linear
+  gap, int32 scores, the full int32 H matrix written to HBM.  Independent
+  pairs, no collective inside the step: weak scaling.
+* c4: 1024 pairs of 4,000 x 4,000 SW (score only), sharded over ranks
+  (shard.ShardedBatch); every step ends with an RCCL all-gather of the scores.
+* c3: one 97,403 x 97,403 banded (|i-j| <= 512) reference-Gotoh fill, H written.
 * c5: one 20k x 20k affine SW fill writing 1 B/cell traceback bits.
 
-Prints ONE JSON line (rank 0) with value = whole-job GCUPS, the roofline of
-the stripe kernel (HIP events around that kernel on its own stream) and the
-reference CPU path timed on this host (bounded sample).
+After the timed steps (outside the timed region) the run is checked: the
+plan's sticky error word must be 0 (every timed step completed its waits), the
+score must equal the CPU oracle's, for c2 the checksum of the whole H matrix
+the timed steps wrote must equal the oracle's, for c4 the gathered scores must
+equal the committed fixture.  Prints ONE JSON line (rank 0) with value =
+whole-job GCUPS, the roofline of the DP kernel (HIP events around that kernel
+on its stream, separate pass) and the reference's CPU method timed on this
+host (oracle/cpu_rowsweep.cpp, p' = 1 and p' = host cores, bounded sample).
 """
 from __future__ import annotations
 
@@ -35,6 +41,11 @@ REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s (spec)
+# MI355X_MICROARCH.md: 256 CUs x 4 SIMD-32 x 2.4 GHz, a wave64 VALU op issues in 2 cycles per SIMD
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # = 78.64 T int32 lane-ops/s
+# algorithmic bytes / ops per cell, fixed up front
+BYTES_PER_CELL = {"c2": 4.0, "c3": 4.0}
+OPS_PER_CELL = {"c4": 8.0, "c5": 12.0}
 
 
 def parse():
@@ -48,52 +59,38 @@ def parse():
     return ap.parse_args()
 
 
-def dataset():
-    from oracle.oracle import load_dataset  # plain FASTA reader of the committed data file
-
-    return load_dataset()[1]
-
-
-def encode(s: bytes) -> np.ndarray:
-    return np.frombuffer(s.translate(bytes.maketrans(b"ACGT", b"\x00\x01\x02\x03")), dtype=np.uint8).copy()
-
-
-def synth(n: int, seed: int) -> bytes:
-    rng = np.random.default_rng(seed)
-    return rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), n).tobytes()
-
-
-def cpu_baseline(workload: str, A: bytes, B: bytes):
-    """The reference's own CPU fill (oracle/_ref, compiled from its sources) on a
-    bounded sample of the workload; the C restatement if _ref is absent."""
+def cpu_baseline(wl: str, A: bytes, B: bytes, cores: int):
+    """The reference's CPU method (row sweep, fresh std::threads per row phase, prefix-max
+    horizontal gap: oracle/cpu_rowsweep.cpp) on this host, p' = 1 and p' = cores, bounded samples."""
     from oracle import oracle as O
 
-    if O.ref_available():
-        L = min(len(A), len(B), 10000)
-        r = O.ref_subproblem(A[:L], B[:L], -1, -1, 1.0, 2.0, p=1, tables=False, traceback=False)
-        secs = r["fill_seconds"]
-        return dict(value=round(L * L / secs / 1e9, 4), unit="GCUPS", cores=1, kind="reference",
-                    sample=f"Subproblem::compute_tables (subproblem_alignment.cpp:329) p'=1 on {L}x{L} "
-                           f"of the same pair, reference sources built -O2 by oracle/Makefile; "
-                           f"{secs:.2f} s fill (table allocation excluded)")
-    L = min(len(A), len(B), 6000)
-    t0 = time.perf_counter()
-    O.sw(A[:L], B[:L], 1, 0, 1, 1)
-    secs = time.perf_counter() - t0
-    return dict(value=round(L * L / secs / 1e9, 4), unit="GCUPS", cores=1, kind="port",
-                sample=f"oracle orc_sw (C restatement) {L}x{L}, {secs:.2f} s")
+    mode = 0 if wl == "c3" else 1  # c3: the reference's own Gotoh recurrence; else SW linear int32
+    L = min(len(A), len(B), 10000)
+    A, B = A[:L], B[:L]
+    pts = []
+    for p, rows in ((1, L), (cores, min(L, 1500))):
+        _, secs = O.rowsweep(A, B, p=p, mode=mode, g=1.0, h=2.0, match=1, mismatch=0, rows=rows)
+        pts.append(dict(threads=p, rows=rows, cols=L, seconds=round(secs, 3), gcups=round(rows * L / secs / 1e9, 4)))
+    best = max(pts, key=lambda x: x["gcups"])
+    return dict(value=best["gcups"], unit="GCUPS", cores=best["threads"], kind="port",
+                sample=f"the reference's CPU method (subproblem_alignment.cpp:251-332 row sweep, prefix-max "
+                       f"T2 :13-103, fresh std::threads per phase) restated in oracle/cpu_rowsweep.cpp, "
+                       f"{'Gotoh' if mode == 0 else 'SW-linear int32'} recurrence on the first rows of the "
+                       f"same pair; p'=1 and p'={cores} (host nproc {os.cpu_count()}, this job's share "
+                       f"{cores}); best shown",
+                points=pts)
 
 
-def load_traffic(workload: str):
-    """Per-launch HBM bytes of the stripe kernel from the committed PMC profile
-    (profiles/<round>_<workload>_pmc.json written by scripts/pmc_summary.py:
-    2 x FETCH_SIZE + WRITE_SIZE, per the MI355X guide's gfx950 correction), or None."""
+def load_traffic(wl: str):
+    """Per-launch HBM bytes of the DP kernel from the newest committed PMC profile
+    (profiles/<round>_<wl>_pmc.json, scripts/pmc_summary.py: 2 x FETCH_SIZE + WRITE_SIZE per the
+    MI355X guide's gfx950 correction), or None."""
     for p in sorted((REPO / "profiles").glob("*_pmc.json"), reverse=True):
         try:
             d = json.loads(p.read_text())
         except Exception:
             continue
-        if d.get("workload") == workload and d.get("hbm_bytes_per_launch"):
+        if d.get("workload") == wl and d.get("hbm_bytes_per_launch"):
             return float(d["hbm_bytes_per_launch"]["total"])
     return None
 
@@ -111,60 +108,44 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     from cse305_parallel_sequence_alignment_amd import _lib as LB
+    from cse305_parallel_sequence_alignment_amd import data
     from cse305_parallel_sequence_alignment_amd.plan import Plan
+    from cse305_parallel_sequence_alignment_amd.shard import ShardedBatch, broadcast_reference
 
-    seqs = None if args.synthetic else dataset()
-
-    def seq(k, L, salt):
-        if seqs is None:
-            return synth(L, 0x5EED0000 + salt * 1000 + k)
-        s = seqs[k % len(seqs)]
-        return s[:L]
-
+    syn = args.synthetic
     wl = args.workload
+    batch = None
     if wl == "c2":
-        m = n = 10000
-        B = seq(0, n, 1)  # the reference sequence (rank 0 owns it, bcast)
-        A = seq(1 + rank, m, 1)
+        A, B = data.c2_pair(rank, syn)
+        m, n = len(A), len(B)
         pairs_m, pairs_n, a_off, b_off = [m], [n], [0], [0]
         plan_kw = dict(alg=LB.SW_LINEAR, cells=LB.CELLS_H, match=1, mismatch=0, gap_open=1, gap_extend=1)
         cells_per_step = m * n
-        algo_bytes_per_cell = 4.0  # int32 H written once
         desc = "sw-linear 10000x10000, match 1 mismatch 0 gap 1, int32 H written"
-        dtype = "int32"
     elif wl == "c3":
-        m = n = 100000
-        B = seq(0, n, 3) if seqs is None else (seqs[3][:97403] + seqs[4][:2597])[:n]
-        A = seq(1 + rank, m, 3) if seqs is None else (seqs[4][:97403] + seqs[3][:2597])[:m]
+        A, B = data.c3_pair(syn)
         m, n = len(A), len(B)
-        pairs_m, pairs_n, a_off, b_off = [m], [n], [0], [0]
         band = 512
+        pairs_m, pairs_n, a_off, b_off = [m], [n], [0], [0]
         plan_kw = dict(alg=LB.NW_BANDED, cells=LB.CELLS_H, match=1, mismatch=0, gap_open=3, gap_extend=1, band=band)
         cells_per_step = sum(min(n, i + band) - max(1, i - band) + 1 for i in range(1, m + 1))
-        algo_bytes_per_cell = 4.0
         desc = f"banded reference Gotoh {m}x{n}, band 512, g=1 h=2, int32 H written"
-        dtype = "int32"
     elif wl == "c5":
-        m = n = 20000
-        B = seq(0, n, 5)
-        A = seq(1 + rank, m, 5)
+        A, B = data.c5_pair(rank, syn)
+        m, n = len(A), len(B)
         pairs_m, pairs_n, a_off, b_off = [m], [n], [0], [0]
         plan_kw = dict(alg=LB.SW_AFFINE, cells=LB.CELLS_DIR, match=1, mismatch=0, gap_open=3, gap_extend=1,
                        track_end=True)
         cells_per_step = m * n
-        algo_bytes_per_cell = 1.0
         desc = "sw-affine 20000x20000, open 3 extend 1, 1 B/cell traceback bits written"
-        dtype = "int32"
     else:  # c4
-        L = 4000
-        total_pairs = 1024
-        per = (total_pairs + world - 1) // world
-        lo, hi = rank * per, min(total_pairs, (rank + 1) * per)
-        B = seq(0, L, 4)
-        rng = np.random.default_rng(0x5EED0004)
-        offs = rng.integers(0, 13309 - L, size=total_pairs)
-        qs = [(seqs[k % 20][offs[k]:offs[k] + L] if seqs is not None else synth(L, 0x5EED0004 + k)) for k in
-              range(lo, hi)]
+        total = data.C4_PAIRS
+        L = data.C4_LEN
+        B = data.c4_reference(syn)
+        from cse305_parallel_sequence_alignment_amd.shard import shard_range
+
+        lo, hi = shard_range(total, rank, world)
+        qs = data.c4_queries(lo, hi, syn)
         A = b"".join(qs)
         pairs_m = [L] * len(qs)
         pairs_n = [L] * len(qs)
@@ -172,27 +153,33 @@ def main():
         b_off = [0] * len(qs)
         plan_kw = dict(alg=LB.SW_LINEAR, cells=LB.CELLS_NONE, match=1, mismatch=0, gap_open=1, gap_extend=1)
         cells_per_step = L * L * len(qs)
-        algo_bytes_per_cell = 0.0
-        desc = f"{total_pairs} x (4000x4000) sw-linear score-only, shard {len(qs)} pairs/rank"
-        dtype = "int32"
+        desc = f"{total} x (4000x4000) sw-linear score-only, {len(qs)} pairs on this rank"
 
-    dA = torch.from_numpy(encode(A)).to(dev)
-    dB = torch.from_numpy(encode(B)).to(dev)
-    if world > 1:
-        dist.broadcast(dB, src=0)  # RCCL: the shared reference sequence
+    dA = torch.from_numpy(data.encode(A)).to(dev)
+    dB = torch.from_numpy(data.encode(B)).to(dev)
+    broadcast_reference(dB)  # RCCL over xGMI: rank 0's reference sequence to every rank (once)
     plan = Plan(cells=plan_kw.pop("cells"), ms=pairs_m, ns=pairs_n, a_offs=a_off, b_offs=b_off, **plan_kw)
     out = torch.empty(max(plan.cells_elems, 1), dtype=torch.uint8 if plan.cells == LB.CELLS_DIR else torch.int32,
                       device=dev) if plan.cells != LB.CELLS_NONE else None
-    score_buf = torch.zeros(1, dtype=torch.int64, device=dev)
-    gathered = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
 
-    def step():
-        plan.run(dA, dB, out)
-        if world > 1:
-            # scores of every rank -> every rank (tiny RCCL all-gather over xGMI)
-            dist.all_gather(gathered, score_buf)
+    if wl == "c4":
+        local_scores = torch.empty(len(pairs_m), dtype=torch.int32, device=dev)
 
-    plan.set_timing(False)  # no event records inside the timed steps (kernel_ms pass below re-enables)
+        def score_block(lo_, hi_):
+            assert (lo_, hi_) == (lo, hi)
+            plan.run(dA, dB, out)
+            plan.scores_into(local_scores)
+            return local_scores
+
+        batch = ShardedBatch(total, rank, world, score_block)
+
+        def step():
+            return batch.step()  # fill this rank's pairs, then RCCL all-gather of every rank's scores
+    else:
+        def step():
+            plan.run(dA, dB, out)
+
+    plan.set_timing(False)  # no event records inside the timed steps (the kernel_ms pass below re-enables)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -201,7 +188,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        gathered = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -211,35 +198,72 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    # ---- checks of what the timed steps produced (outside the timed region) ----
+    err = plan.error()
+    if err:
+        raise SystemExit(f"rank {rank}: a kernel wait hit its spin limit (site {err}) during the timed steps")
     res = plan.results()
-    # stripe-kernel duration from HIP events on the launch stream (separate pass)
+    from oracle import oracle as O  # CPU checker
+
+    checks = {}
+    if wl == "c2":
+        o = O.sw(A, B, 1, 0, 1, 1, want_h=(rank == 0))
+        checks["score_matches_cpu"] = bool(o["score"] == res[0]["score"])
+        if rank == 0:
+            checks["h_matches_cpu"] = bool(plan.checksum(out) == O.checksum_h(o["H"]))
+            del o
+    elif wl == "c5":
+        o = O.sw(A, B, 1, 0, 3, 1)
+        checks["score_matches_cpu"] = bool(o["score"] == res[0]["score"] and tuple(o["end"]) == tuple(res[0]["end"]))
+    elif wl == "c3":
+        checks["score_matches_cpu"] = bool(int(O.banded_ref(A, B, 512, 1.0, 2.0)) == res[0]["score"])
+    else:
+        got = [int(x) for x in gathered.cpu().tolist()]
+        fx = REPO / "tests" / "golden" / "c4_scores.json"
+        if not syn and fx.exists():
+            checks["scores_match_fixture"] = got == json.loads(fx.read_text())["scores"]
+        checks["score_rank_block_matches_cpu_sample"] = all(
+            got[lo + k] == O.sw(qs[k], B, 1, 0, 1, 1)["score"] for k in (0, len(qs) // 2, len(qs) - 1) if qs)
+    ok = torch.tensor([int(all(checks.values()))], dtype=torch.int32, device=dev)
+    if world > 1:
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+
+    # DP-kernel duration from HIP events on the launch stream (separate pass; same plan and buffers)
     kms = []
     plan.set_timing(True)
     for _ in range(max(3, min(args.steps, 10))):
         plan.run(dA, dB, out)
         kms.append(plan.kernel_ms())
     kern_ms = float(np.mean(kms))
+    if plan.error():
+        raise SystemExit(f"rank {rank}: a kernel wait hit its spin limit in the timing pass")
 
     total_cells = cells_per_step * args.steps * world
     gcups = total_cells / elapsed / 1e9
     if rank == 0:
-        achieved = algo_bytes_per_cell * cells_per_step / (kern_ms * 1e-3) / 1e9
-        traffic = load_traffic(wl)
-        roof = dict(bound="hbm", achieved=round(achieved, 2), peak=HBM_PEAK_GBS, unit="GB/s",
-                    frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
-                    note="algorithmic bytes = %.0f B/cell x cells / DP-kernel time (flow_kernel for C2); bound by the "
-                         "per-wave DP dependency chain of the anti-diagonal wavefront, not by HBM (DESIGN.md)"
-                         % algo_bytes_per_cell)
+        kern_gcups = cells_per_step / (kern_ms * 1e-3) / 1e9
+        if wl in BYTES_PER_CELL:
+            achieved = BYTES_PER_CELL[wl] * kern_gcups
+            roof = dict(bound="hbm", achieved=round(achieved, 2), peak=HBM_PEAK_GBS, unit="GB/s",
+                        frac=round(achieved / HBM_PEAK_GBS, 4), traffic=load_traffic(wl),
+                        note=f"algorithmic bytes = {BYTES_PER_CELL[wl]:.0f} B/cell x {cells_per_step} cells per "
+                             f"launch / DP-kernel mean time {kern_ms:.4f} ms (HIP events on the launch stream); "
+                             f"traffic = committed PMC HBM bytes per launch. The kernel is bound by the "
+                             f"wavefront's dependency chain, not by HBM (DESIGN.md)")
+        else:
+            achieved = OPS_PER_CELL[wl] * kern_gcups / 1000.0
+            roof = dict(bound="valu", achieved=round(achieved, 3), peak=round(VALU_PEAK_TOPS, 2),
+                        unit="T int32 lane-ops/s", frac=round(achieved / VALU_PEAK_TOPS, 4),
+                        traffic=load_traffic(wl),
+                        note=f"algorithmic ops = {OPS_PER_CELL[wl]:.0f} int32 ops/cell (SURVEY §8(d)) x cells / "
+                             f"DP-kernel mean time {kern_ms:.4f} ms; peak = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz")
         cpu = None
         if not args.no_cpu_baseline:
             try:
-                cpu = cpu_baseline(wl, A[:m] if wl != "c4" else A[:4000], B)
+                cpu = cpu_baseline(wl, A[:data.C4_LEN] if wl == "c4" else A, B, min(16, os.cpu_count() or 1))
             except Exception as e:  # pragma: no cover
-                cpu = dict(value=None, unit="GCUPS", cores=1, kind="reference", sample=f"failed: {e}")
-        score_ok = None
-        if wl == "c2":
-            from oracle import oracle as O  # CPU checker for the max score
-            score_ok = bool(O.sw(A, B, 1, 0, 1, 1)["score"] == res[0]["score"])
+                cpu = dict(value=None, unit="GCUPS", cores=1, kind="port", sample=f"failed: {e}")
         line = {
             "metric": "GCUPS (DP cell updates/s) + max-score match vs CPU, 10k×10k SW",
             "value": round(gcups, 3),
@@ -251,19 +275,23 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": dtype,
-            "data": "synthetic i.i.d. ACGT" if seqs is None else "gene_sequences_test (reference's bundled FASTA)",
-            "config": {"workload": wl + ": " + desc, "cells_per_step_per_gpu": int(cells_per_step),
-                       "parallelism": f"dp{world} (one pair per GPU; RCCL bcast of the reference + all-gather)"
-                       if wl != "c4" else f"dp{world} (pairs sharded over GPUs)",
-                       "score_rank0": int(res[0]["score"]), "score_matches_cpu": score_ok,
-                       "stripe_kernel_ms": round(kern_ms, 4)},
+            "dtype": "int32",
+            "data": "synthetic i.i.d. ACGT" if syn else "gene_sequences_test (reference's bundled FASTA)",
+            "config": dict(workload=wl + ": " + desc, cells_per_step_per_gpu=int(cells_per_step),
+                           parallelism=(f"dp{world} (pairs sharded over GPUs; RCCL bcast of the reference, "
+                                        f"all-gather of scores every step)" if wl == "c4" else
+                                        f"dp{world} (one independent pair per GPU; RCCL bcast of the reference "
+                                        f"once; no collective in the step)"),
+                           score_rank0=int(res[0]["score"]), checks_all_ranks=bool(ok.item()), **checks,
+                           kernel_errors=0, dp_kernel_ms=round(kern_ms, 4)),
             "roofline": roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if not bool(ok.item()):
+        raise SystemExit(f"rank {rank}: result check failed: {checks}")
 
 
 if __name__ == "__main__":

@@ -13,7 +13,7 @@ import os
 from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
-LIB_PATH = Path(os.environ.get("MSA_LIB_PATH", PKG / "libmsa.so"))  # override: diagnostic builds only
+LIB_PATH = PKG / "libmsa.so"
 
 MSA_OK = 0
 STATUS = {
@@ -86,6 +86,9 @@ def lib() -> C.CDLL:
     L.msa_plan_cells_size.argtypes = [P, C.POINTER(i64)]
     L.msa_plan_run.argtypes = [P, P, P, P, P, P, P]
     L.msa_plan_results.argtypes = [P, P, P]
+    L.msa_plan_error.argtypes = [P, C.POINTER(C.c_int), P]
+    L.msa_plan_clear_error.argtypes = [P, P]
+    L.msa_plan_scores.argtypes = [P, P, P]
     L.msa_plan_stripe_meta.argtypes = [P, P, i64, P]
     L.msa_plan_stripes.argtypes = [P]
     L.msa_plan_stripes.restype = i64
@@ -114,7 +117,8 @@ class _Bind:
 EXPORTED = [
     "msa_status_string", "msa_version", "msa_device_count", "msa_main_alignment", "msa_subproblem",
     "msa_partial_partition", "msa_partial_tables", "msa_plan_create", "msa_plan_destroy", "msa_plan_cells_size",
-    "msa_plan_run", "msa_plan_results", "msa_plan_stripe_meta", "msa_plan_stripes", "msa_plan_pair_layout",
+    "msa_plan_run", "msa_plan_results", "msa_plan_error", "msa_plan_clear_error", "msa_plan_scores",
+    "msa_plan_stripe_meta", "msa_plan_stripes", "msa_plan_pair_layout",
     "msa_plan_checksum",
     "msa_plan_last_kernel_ms", "msa_plan_set_timing", "msa_encode_pair", "msa_sw_align",
 ]

@@ -113,22 +113,15 @@ kfn_t pick_kernel(int alg, int out, int tp, bool sgl) {
 
 // single-pair SW linear (msa_flow.hip): pass 1 (chain), pass 2 (fill + H)
 kfn_t pick_flow(int alg, bool best, bool save, int tp, int R) {
+  // score-only plans: pass 1 alone, one row per lane, best cell tracked in the chain;
+  // H plans: pass 1 + in-launch pass 2, two rows per lane
   const bool fl = (alg == MSA_ALG_SWL);
   if (best) return fl ? flow_kernel<true, true, false, false> : flow_kernel<false, true, false, false>;
   if (save && R == 2) {
     if (fl) return tp ? flow_kernel<true, false, true, true, 2> : flow_kernel<true, false, true, false, 2>;
     return tp ? flow_kernel<false, false, true, true, 2> : flow_kernel<false, false, true, false, 2>;
   }
-  if (save) {
-    if (fl) return tp ? flow_kernel<true, false, true, true> : flow_kernel<true, false, true, false>;
-    return tp ? flow_kernel<false, false, true, true> : flow_kernel<false, false, true, false>;
-  }
   return nullptr;
-}
-
-int env_int(const char* name, int dflt) {
-  const char* v = std::getenv(name);
-  return (v && *v) ? std::atoi(v) : dflt;
 }
 
 }  // namespace
@@ -161,7 +154,9 @@ struct msa_plan {
   // device
   msa_pair_desc* d_pairs = nullptr;
   msa_stripe_meta* d_meta = nullptr;
-  int* d_ticket = nullptr;  // [0] ticket, [1] err
+  int* d_ticket = nullptr;  // [0] ticket, [4..11] per-XCD item chunks, [12] pass-2 blocks (reset every run)
+  int* d_err = nullptr;     // sticky error word: set by a kernel wait that hit its spin limit; cleared
+                            // only at plan creation and by msa_plan_clear_error
   unsigned long long* d_gbuf = nullptr;
   uint8_t* d_cod = nullptr;                // MSA_NCOPY byte-shifted padded column-code copies
   msa_pair_desc* d_segs = nullptr;         // distinct column sequences (b_off, n, cod_off)
@@ -238,11 +233,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   int kalg;
   switch (alg) {
     case MSA_SW_LINEAR:
-#ifdef MSA_NO_SWL0
-      kalg = MSA_ALG_SWL;
-#else
       kalg = (desc->match >= 0 && desc->mismatch >= 0) ? MSA_ALG_SWL0 : MSA_ALG_SWL;
-#endif
       break;
     case MSA_SW_AFFINE: kalg = MSA_ALG_SWA; break;
     case MSA_NW_BANDED: kalg = MSA_ALG_NWA; break;
@@ -255,17 +246,14 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   // A banded pair has only ~(2*band+64)/(64*lag) stripes in flight at once:
   // one workgroup cycling its waves over all stripes (the batch kernel, wrap
   // link through the LDS row buffer) beats a chain of cross-workgroup hand-offs.
-  bool single = desc->single != 0;
-#ifdef MSA_BANDED_BATCH
-  if (single && kalg == MSA_ALG_NWA && desc->band >= 0 && (int64_t)desc->band * 2 + 64 < desc->n[0] / 4) single = false;
-#endif
+  const bool single = desc->single != 0;
   P->d.single = single ? 1 : 0;
-  // flow kernel: one SW-linear pair whose 8 LDS code copies fit next to the rings
-  // two-pass flow kernels: one SW-linear pair whose 8 LDS code copies fit next to the rings
+  // flow kernels: one SW-linear pair whose 8 LDS code copies fit next to the rings
+  // (n <= ~19.5k columns); wider pairs run the one-pass stripe kernel
   const size_t flow_lds = (size_t)(FL_FLAGS + (FL_W + 1) * 256) * 4 + (size_t)FL_NCOPY * fl_code_bytes((int)desc->n[0]);
   const bool flow = single && (kalg == MSA_ALG_SWL || kalg == MSA_ALG_SWL0) &&
-                    (out_mode == MSA_OUT_H || (out_mode == MSA_OUT_NONE && !tp)) &&
-                    env_int("MSA_FLOW", 1) != 0 && desc->m[0] > 0 && flow_lds <= 160 * 1024;
+                    (out_mode == MSA_OUT_H || (out_mode == MSA_OUT_NONE && !tp)) && desc->m[0] > 0 &&
+                    flow_lds <= 160 * 1024;
   P->flow = flow;
   P->flow2 = flow && out_mode == MSA_OUT_H;
   const int W = flow ? FL_W : (single ? MSA_WAVES_SINGLE : MSA_WAVES_BATCH);
@@ -274,7 +262,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   P->KS = KS;
   P->threads = (flow ? W + 2 : W + 1 + (single ? 1 : 0)) * 64;
   // rows per lane of the flow kernel (two-pass plans): 2 halves the inter-wave hand-offs per row
-  P->R = (flow && out_mode == MSA_OUT_H) ? std::max(1, std::min(2, env_int("MSA_R", 2))) : 1;
+  P->R = (flow && out_mode == MSA_OUT_H) ? 2 : 1;
   P->fn = flow ? pick_flow(kalg, out_mode == MSA_OUT_NONE, out_mode == MSA_OUT_H, tp, P->R)
                : pick_kernel(kalg, out_mode, tp, single);
   if (!P->fn) { delete P; return MSA_ERR_UNSUPPORTED; }
@@ -422,6 +410,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   if (hipMemset(P->d_meta, 0, sizeof(msa_stripe_meta) * std::max<int64_t>(1, P->total_stripes)) != hipSuccess)
     return fail();
   if (hipMalloc(&P->d_ticket, 64) != hipSuccess) return fail();
+  if (hipMalloc(&P->d_err, 64) != hipSuccess || hipMemset(P->d_err, 0, 64) != hipSuccess) return fail();
   if (hipMalloc(&P->d_cod, (size_t)MSA_NCOPY * P->cod_copy + 64) != hipSuccess) return fail();
   if (hipMalloc(&P->d_segs, sizeof(msa_pair_desc) * P->segs.size()) != hipSuccess) return fail();
   if (hipMemcpy(P->d_segs, P->segs.data(), sizeof(msa_pair_desc) * P->segs.size(), hipMemcpyHostToDevice) !=
@@ -468,6 +457,7 @@ void msa_plan_destroy(msa_plan* P) {
   if (P->d_pairs) (void)hipFree(P->d_pairs);
   if (P->d_meta) (void)hipFree(P->d_meta);
   if (P->d_ticket) (void)hipFree(P->d_ticket);
+  if (P->d_err) (void)hipFree(P->d_err);
   if (P->d_gbuf) (void)hipFree(P->d_gbuf);
   if (P->d_cod) (void)hipFree(P->d_cod);
   if (P->d_segs) (void)hipFree(P->d_segs);
@@ -515,7 +505,7 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
   a.pairs = P->d_pairs;
   a.meta = P->d_meta;
   a.ticket = P->d_ticket;
-  a.err = P->d_ticket + 1;
+  a.err = P->d_err;
   a.gbuf = P->d_gbuf;
   a.gbuf_stride = P->gbuf_stride;
   if (P->d.cells == MSA_CELLS_DIR) a.outDir = (uint8_t*)c0;
@@ -532,7 +522,7 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
   a.nflow = P->nflow;
   a.brw = P->brw;
   a.nseg = P->nseg;
-  a.nblk = env_int("MSA_NOFILL", 0) ? 0 : P->nblk;  // (diagnostic: pass 1 alone)
+  a.nblk = P->nblk;
   {
     const unsigned virt = (P->kp.alg == MSA_ALG_SWL || P->kp.alg == MSA_ALG_SWL0 || P->kp.alg == MSA_ALG_SWA) ? MSA_VIRT_CODE : 0u;
     hipLaunchKernelGGL(stage_codes_kernel, dim3(64, (unsigned)P->segs.size()), dim3(256), 0, st, dB, P->d_segs,
@@ -579,15 +569,38 @@ int msa_plan_last_kernel_ms(msa_plan* P, float* ms) {
 int msa_plan_results(msa_plan* P, msa_pair_result* out, void* stream) {
   if (!P || !out) return MSA_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
-  int err[2] = {0, 0};
-  HIPCHK(hipMemcpyAsync(err, P->d_ticket, sizeof(err), hipMemcpyDeviceToHost, st));
+  int err = 0;
+  HIPCHK(hipMemcpyAsync(&err, P->d_err, sizeof(err), hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(out, P->d_res, sizeof(PairResult) * P->d.n_pairs, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   static_assert(sizeof(PairResult) == sizeof(msa_pair_result), "result layout");
-  if (err[1]) {
-    std::fprintf(stderr, "msa: a kernel wait hit its spin limit (site %d)\n", err[1]);
+  if (err) {
+    std::fprintf(stderr, "msa: a kernel wait hit its spin limit (site %d) in a run since the plan was created "
+                 "or last cleared\n", err);
     return MSA_ERR_TIMEOUT;
   }
+  return MSA_OK;
+}
+
+int msa_plan_error(msa_plan* P, int* code, void* stream) {
+  if (!P || !code) return MSA_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  HIPCHK(hipMemcpyAsync(code, P->d_err, sizeof(int), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  return MSA_OK;
+}
+
+int msa_plan_clear_error(msa_plan* P, void* stream) {
+  if (!P) return MSA_ERR_ARG;
+  HIPCHK(hipMemsetAsync(P->d_err, 0, sizeof(int), (hipStream_t)stream));
+  return MSA_OK;
+}
+
+int msa_plan_scores(msa_plan* P, int32_t* dst, void* stream) {
+  if (!P || !dst) return MSA_ERR_ARG;
+  // the score field of every PairResult, device to device (no host sync)
+  HIPCHK(hipMemcpy2DAsync(dst, sizeof(int32_t), P->d_res, sizeof(PairResult), sizeof(int32_t), (size_t)P->d.n_pairs,
+                          hipMemcpyDeviceToDevice, (hipStream_t)stream));
   return MSA_OK;
 }
 

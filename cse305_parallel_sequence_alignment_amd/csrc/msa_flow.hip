@@ -48,11 +48,7 @@ namespace msa {
 #ifndef FL_PS
 #define FL_PS 8         // phases per pass-2 segment (pass 1 saves its state every FL_PS phases)
 #endif
-#ifdef FL_DBG
-#define FL_SPIN_MAX (1u << 16)
-#else
 #define FL_SPIN_MAX (1u << 26)  // a spin limit sets err = the site's code (10..15) instead of hanging
-#endif
 #ifndef FL_PF
 #define FL_PF 12        // step of a phase at which the next phase's inputs are read
 #endif
@@ -92,17 +88,6 @@ __device__ __forceinline__ void lds_vstore(int* p, int v) { *(volatile lds_int*)
 #define FL_CBAR() asm volatile("" ::: "memory")
 // Diagnostic build (-DMSA_STAMPS): stamps[((item*16 + w)*4096 + q)*4 + slot], q = 0:
 //   slot 0: s_memrealtime at the stripe's start, 1: at its end, 2: slow-path phases
-#if defined(MSA_STAMPS) && defined(FL_DBG)
-// live progress probe into host-mapped memory: [block][wave][field]
-#define FL_PROBE(f_, v_)                                                                                   \
-  do {                                                                                                     \
-    if (a.stamps && lane == __builtin_amdgcn_readfirstlane(lane))                                         \
-      __hip_atomic_store(a.stamps + ((size_t)blockIdx.x * 8 + (threadIdx.x >> 6)) * 4 + (f_),              \
-                         (unsigned long long)(v_), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);           \
-  } while (0)
-#else
-#define FL_PROBE(f_, v_) do {} while (0)
-#endif
 #ifdef MSA_STAMPS
 #define FL_STAMP(q_, slot_, v_)                                                                        \
   do {                                                                                              \
@@ -149,37 +134,11 @@ template <int N = 0>
 __device__ __forceinline__ void lgkm_wait_v(fl_v4i (&in)[4], fl_v4u& cw) {
   asm volatile("s_waitcnt lgkmcnt(%5)" : "+v"(in[0]), "+v"(in[1]), "+v"(in[2]), "+v"(in[3]), "+v"(cw) : "i"(N) : "memory");
 }
-// Lane 63 alone: its 16 bottom-row values -> ring block, then the phase
-// counter (DS ops of one wave execute in order: the block lands first).
-// s_nop 4: an SALU exec write needs 5 wait states before a DPP op.
-__device__ __forceinline__ void ds_handoff(unsigned long long m63, unsigned ra, fl_v4i x0, fl_v4i x1, fl_v4i x2,
-                                           fl_v4i x3, unsigned pa, int pv) {
-  unsigned long long sv;
-  asm volatile(
-      "s_mov_b64 %[sv], exec\n\t"
-      "s_mov_b64 exec, %[m]\n\t"
-      "ds_write_b128 %[ra], %[x0]\n\t"
-      "ds_write_b128 %[ra], %[x1] offset:16\n\t"
-      "ds_write_b128 %[ra], %[x2] offset:32\n\t"
-      "ds_write_b128 %[ra], %[x3] offset:48\n\t"
-      "ds_write_b32 %[pa], %[pv]\n\t"
-      "s_mov_b64 exec, %[sv]\n\t"
-      "s_nop 4"
-      : [sv] "=&s"(sv)
-      : [m] "s"(m63), [ra] "v"(ra), [x0] "v"(x0), [x1] "v"(x1), [x2] "v"(x2), [x3] "v"(x3), [pa] "v"(pa),
-        [pv] "v"(pv)
-      : "memory");
-}
-
-#ifdef FL_X_NOHAND
-__device__ __forceinline__ void ds_handoff_lite(unsigned long long m63, unsigned pa, int pv) {
-  unsigned long long sv;
-  asm volatile("s_mov_b64 %[sv], exec\n\ts_mov_b64 exec, %[m]\n\tds_write_b32 %[pa], %[pv]\n\ts_mov_b64 exec, %[sv]\n\ts_nop 4"
-               : [sv] "=&s"(sv) : [m] "s"(m63), [pa] "v"(pa), [pv] "v"(pv) : "memory");
-}
-#endif
-// Same hand-off with 16 ds_write_addtid_b32 (LDS[M0 + offset + 4*lane]; lane 63:
-// M0 = slot - 252): cheaper to issue than four single-lane b128 writes.
+// Lane 63 alone: its 16 bottom-row values -> ring block as 16 ds_write_addtid_b32
+// (LDS[M0 + offset + 4*lane]; lane 63: M0 = slot - 252; cheaper to issue than
+// four single-lane b128 writes), then the phase counter (DS ops of one wave
+// execute in order: the block lands first).  s_nop 4: an SALU exec write needs
+// 5 wait states before a DPP op.
 __device__ __forceinline__ void ds_handoff_tid(unsigned long long m63, unsigned m0v, const int (&x)[16], unsigned pa,
                                                int pv) {
   unsigned long long sv;
@@ -288,7 +247,6 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         int t = 0;
         if (lane == 0) t = atomicAdd(a.ticket + 12, 1);
         t = __builtin_amdgcn_readlane(t, 0);
-        FL_PROBE(0, 2000 + t);
         if (t >= a.nblk) break;
         const FillArgs f{a.A, a.cod, a.br, a.snap, a.outH, a.blk, a.err, a.cod_copy, a.pairs[0].a_off,
                          a.pairs[0].cod_off, a.pairs[0].out_off, a.pairs[0].m, a.pairs[0].n, a.pairs[0].pmax,
@@ -318,7 +276,6 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
     if (threadIdx.x >= 16 && threadIdx.x < 128) flags[threadIdx.x] = 0;
     __syncthreads();
     const int item = uni(flags[0]);
-    FL_PROBE(0, 1000 + item);
     if (item >= kp.n_items) break;
     const int k0 = item * W;
 
@@ -352,11 +309,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         }
         Yr = max(Yr, Y1);
       };
-#ifdef FL_PRELOAD
-      load_codes(L8);
-#else
       load_codes(1024);
-#endif
       const unsigned long long* g_in = a.gbuf + (size_t)(item > 0 ? item - 1 : 0) * a.gbuf_stride;
       int b = 0;
       int consv = 0;
@@ -573,7 +526,6 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
           __attribute__((always_inline)) {
         constexpr bool MASK = decltype(MASK_)::value;  // phase q+1 may lie past the producer's last block
         const int need = MASK ? min(q + 1, Bin + 1) : q + 1;
-        FL_PROBE(2, q);
         if (pubv - dq_in < need) {
 #ifdef MSA_STAMPS
           ++nslow;
@@ -636,15 +588,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         const bool wr = has_out && bq >= 0;
         if (wr && consv < bq - (FL_RINGB - 1)) refresh_cons(bq - (FL_RINGB - 1));
         const unsigned wa = wr ? a_ring_out + (unsigned)((bq & (FL_RINGB - 1)) * 64) : a_dummy;
-#if !defined(FL_B128) && !defined(FL_X_NOHAND)
-        ds_handoff_tid(m63, wa - 252u, xo, a_prog_me, q + 1);  // (-6.5% on C2 vs four b128 writes)
-#elif !defined(FL_X_NOHAND)
-        ds_handoff(m63, wa, fl_v4i{xo[0], xo[1], xo[2], xo[3]}, fl_v4i{xo[4], xo[5], xo[6], xo[7]},
-                   fl_v4i{xo[8], xo[9], xo[10], xo[11]}, fl_v4i{xo[12], xo[13], xo[14], xo[15]}, a_prog_me, q + 1);
-#else
-        asm volatile("" :: "v"(xo[0]), "v"(xo[5]), "v"(xo[10]), "v"(xo[15]));
-        ds_handoff_lite(m63, a_prog_me, q + 1);
-#endif
+        ds_handoff_tid(m63, wa - 252u, xo, a_prog_me, q + 1);  // (-6.5% on C2 vs four single-lane b128 writes)
 #ifdef MSA_STAMPS
         if (q == dq) FL_STAMP(0, 3, __builtin_amdgcn_s_memrealtime());
 #endif
@@ -678,7 +622,6 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
       lgkm_wait_v<0>(INa, CWa);
       lgkm_wait_v<0>(INb, CWb);
       FL_STAMP(0, 1, __builtin_amdgcn_s_memrealtime());
-      FL_PROBE(1, 7777);
       FL_STAMP(0, 2, (unsigned long long)nslow);
       // ---- stripe finalize ----
       msa_stripe_meta* md = a.meta + pd.stripe0 + k;
@@ -702,10 +645,8 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         md->phases = P;
       }
     }
-    FL_PROBE(1, 8888);
     __syncthreads();
   }
-  FL_PROBE(1, 9999);
 }
 
 // Pass 2: block (stripe s, segment seg) of FL_PS phases, one wave.  Its inputs
@@ -720,9 +661,6 @@ __device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, 
   const int m = a.m, n = a.n, S = (m + 64 * R - 1) / (64 * R), g = a.g;
   const int s = blk / a.nseg, seg = blk - s * a.nseg;
   int bb = INT32_MIN, bi = 0, bj = 0;
-#if defined(FL_EXP) && FL_EXP == 1
-  return;
-#endif
   if (s < S) {
     const int P = fl_P(s, m, n, R);
     const int q0 = seg * FL_PS;
@@ -775,10 +713,6 @@ __device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, 
         q1 = q0;  // nothing computed; the block reports no cell
       }
       FL_CBAR();  // (one wave's LDS ops execute in order: the reads below see the writes)
-#if defined(FL_EXP) && FL_EXP == 2
-      if (lane == 0) a.blk[blk] = make_int4(X, U, 0, 0);
-      return;
-#endif
       // column codes: lane r needs columns cs - r + t; column c sits in global copy
       // (c-1+CPAD)&15 at byte (c-1+CPAD) & ~15: one aligned dwordx4 per phase
       const int b0 = cs - lane - 1 + MSA_CPAD;

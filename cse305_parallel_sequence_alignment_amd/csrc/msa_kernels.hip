@@ -383,7 +383,7 @@ __device__ __forceinline__ void gstore(unsigned long long* p, unsigned long long
 // Cell-output stores (H / T2 / T3 / direction planes) are written once and
 // never read back by the kernel: non-temporal stores stream them at ~64 B/clk
 // per CU, where plain (write-allocate) stores saturate at ~8 B/clk per CU --
-// below what four stripe waves produce (scratch/stbw.hip measurement).
+// below what four stripe waves produce (mbench/mb_store.hip measurement).
 typedef int msa_v4i __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void ntstore(int4* p, int4 v) {
   const msa_v4i x = {v.x, v.y, v.z, v.w};
@@ -395,22 +395,13 @@ enum Snk { SNK_NONE = 0, SNK_RING = 1, SNK_ROW = 2, SNK_GLOBAL = 3 };
 
 // Loader wave (wave W): in single mode it pulls the row above the
 // item's first stripe from the previous workgroup's granules (HBM, `sc1`)
-// into the LDS staging ring MSA_LOAD_AHEAD phases ahead, so no compute wave
-// ever waits on a global load.  Prefetch slots are compile-time indices
-// (loop unrolled by MSA_LOAD_AHEAD): no register rotation, hence no forced
-// vmcnt(0) right after a load.
-#ifndef MSA_LOAD_AHEAD
-#define MSA_LOAD_AHEAD 2
-#endif
+// into the LDS staging ring one phase ahead, so no compute wave ever waits
+// on a global load.
 
 // Phase barrier.  The diagnostic build (-DMSA_STAMPS) records s_memtime just
 // before and after every barrier of every wave: stamps[((item*16 + wave)*4096
 // + phase)*2 + {0,1}] (phases >= 4096 and items >= 64 are not recorded).
-#ifdef MSA_DBG_NO_SYNC
-#define MSA_BARRIER_() do {} while (0)  // timing experiments only: results are garbage
-#else
 #define MSA_BARRIER_() __syncthreads()
-#endif
 #ifdef MSA_STAMPS
 #ifdef MSA_STAMPS_RT
 #define MSA_CLOCK() __builtin_amdgcn_s_memrealtime()  // chip-wide 100 MHz: comparable across XCDs
@@ -479,7 +470,6 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
   // virtual code whose score (MSA_VIRT_SCORE) keeps every out-of-matrix cell
   // strictly below a real cell, so the plain recurrence runs over them.
   constexpr bool SWK = (swlin(ALG) || ALG == MSA_ALG_SWA);
-  constexpr int LA = (MSA_LOAD_AHEAD * 16 + KS - 1) / KS;  // loader prefetch depth in phases
   extern __shared__ __attribute__((aligned(16))) int smem[];
   const msa_kparams& kp = a.kp;
   const int lane = threadIdx.x & 63;
@@ -704,11 +694,10 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
 #pragma unroll
         for (int h = 0; h < CPP; ++h) commit_border(h);
       }
-#ifndef MSA_LOADER_PREFETCH
       // Just-in-time staging: during phase p the loader issues the granule
       // loads of phase p+1, then waits for them (one global round trip fits
       // in a phase) and commits -- the producer only has to be one phase plus
-      // the store->load visibility ahead, instead of LA+1 phases.
+      // the store->load visibility ahead.
       unsigned long long G[CPP];
       if (act) {
         {
@@ -750,61 +739,6 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
         }
         MSA_SYNC(p);
       }
-#else
-      constexpr int NS = LA * CPP;  // prefetch slots; slot c % NS holds the load of chunk c
-      unsigned long long G[NS];
-      if (act) {
-        // start only once the producer is LA+1 phases ahead, so that every
-        // prefetch below reads an already-published granule (no re-poll stalls)
-        {
-          const int cw_ = min(nch0 - 1, (LA + 2) * CPP - 1);
-          const int colw = min(min(s0.cs + 16 * cw_ + 15, chi), n);
-          unsigned spins = 0;
-          while ((unsigned)(gload(g_in + colw + MSA_GOFF) >> 32) != ep) {
-            __builtin_amdgcn_s_sleep(2);
-            if (++spins > (1u << 24)) {
-              if (lane == 0) atomicExch(a.err, 1);
-              break;
-            }
-          }
-        }
-#pragma unroll
-        for (int c = 0; c < NS; ++c) G[c] = loader_issue<NC>(a, s0.cs, c, g_in, lane);
-#pragma unroll
-        for (int h = 0; h < CPP; ++h) {
-          loader_commit<NC>(a, s0.cs, nch0, h, G[h], g_in, stage, chi, n, ep, lane);
-          G[h] = loader_issue<NC>(a, s0.cs, NS + h, g_in, lane);
-        }
-      }
-      __syncthreads();  // phase 0 staged before any compute wave reads it
-      for (int ph = 0; ph < total; ph += LA) {
-#pragma unroll
-        for (int s = 0; s < LA; ++s) {
-          const int p = ph + s;
-          if (p < total) {
-
-            if (act) {
-              if (p + 1 < s0.P) {
-#pragma unroll
-                for (int h = 0; h < CPP; ++h) {
-                  const int c = (p + 1) * CPP + h;
-                  const int slot = ((s + 1) % LA) * CPP + h;
-                  loader_commit<NC>(a, s0.cs, nch0, c, G[slot], g_in, stage, chi, n, ep, lane);
-                  if (c + NS < nch0) G[slot] = loader_issue<NC>(a, s0.cs, c + NS, g_in, lane);
-                }
-              }
-            } else if (border) {
-              if (p + 1 < s0.P) {
-#pragma unroll
-                for (int h = 0; h < CPP; ++h) commit_border((p + 1) * CPP + h);
-              }
-            }
-            sink_phase(p - 1 - sl.T);  // the last stripe's phase completed by the previous barrier
-            MSA_SYNC(p);
-          }
-        }
-      }
-#endif
       sink_phase(total - 1 - sl.T);
       continue;
     }
@@ -948,11 +882,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
           for (int v = 0; v < NC; ++v) {
 #pragma unroll
             for (int u = 0; u < KS / 4; ++u) {
-#ifdef MSA_DBG_NO_IN
-              const int4 x = make_int4(q, q + 1, q + 2, u);
-#else
               const int4 x = *reinterpret_cast<const int4*>(base + v * in_vs + 4 * u);
-#endif
               IN[v][4 * u + 0] = x.x; IN[v][4 * u + 1] = x.y; IN[v][4 * u + 2] = x.z; IN[v][4 * u + 3] = x.w;
             }
           }
@@ -971,11 +901,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
         if constexpr (LDSCODE) load_codes(q);
 #pragma unroll
         for (int u = 0; u < KS / 4; ++u) {
-#ifdef MSA_DBG_NO_CW
-          cw[u] = (unsigned)(lane + q * 0x01010101 + u) & 0x03030303u;
-#else
           cw[u] = cwn[u];
-#endif
         }
 #ifdef MSA_STAMPS
         {
@@ -985,9 +911,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
           MSA_MARK(ph + q, 3);
         }
 #endif
-#ifndef MSA_DBG_NO_CW
         if constexpr (!LDSCODE) load_codes(q + 1);
-#endif
         int hist[NC][KS];
         int hv[KS];
         unsigned dirw[KS / 4];
@@ -1066,11 +990,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
         MSA_MARK(ph + q, 2);
         // hand the bottom row to the next stripe: lane 63, once per phase
         if constexpr (SHREG) {
-#ifdef MSA_DBG_NO_RING
-          if (snk == SNK_GLOBAL && lane >= 64 - KS) {  // keep cross-workgroup publishes
-#else
           if (snk != SNK_NONE && lane >= 64 - KS) {
-#endif
             const int kk_ = lane - (64 - KS);
             if (snk == SNK_GLOBAL) {
               // last stripe of the item: publish straight to the next workgroup

@@ -86,15 +86,58 @@ class Plan:
         except Exception:
             pass
 
+    def _check_buffers(self, dA, dB, outs):
+        """The C-ABI takes raw device pointers: check device, dtype, contiguity and sizes here, so an
+        undersized or misplaced buffer raises instead of letting a kernel read or write out of bounds."""
+        import torch
+
+        need_a = max(o + m for o, m in zip(self._arrs[2], self.ms))
+        need_b = max(o + n for o, n in zip(self._arrs[3], self.ns))
+        for name, t, need in (("dA", dA, need_a), ("dB", dB, need_b)):
+            if t is None or not t.is_cuda or t.dtype != torch.uint8 or not t.is_contiguous():
+                raise ValueError(f"{name} must be a contiguous uint8 CUDA tensor of codes")
+            if t.numel() < need:
+                raise ValueError(f"{name} holds {t.numel()} codes, the plan reads {need}")
+        planes = {LB.CELLS_NONE: 0, LB.CELLS_H: 1, LB.CELLS_DIR: 1, LB.CELLS_TAB: 3}[self.cells]
+        want = torch.uint8 if self.cells == LB.CELLS_DIR else torch.int32
+        for k, t in enumerate(outs):
+            if k >= planes:
+                continue
+            if t is None or not t.is_cuda or t.dtype != want or not t.is_contiguous():
+                raise ValueError(f"out{k} must be a contiguous {want} CUDA tensor")
+            if t.numel() < self.cells_elems:
+                raise ValueError(f"out{k} holds {t.numel()} elements, the plan writes {self.cells_elems}")
+
     def run(self, dA, dB, out0=None, out1=None, out2=None, stream=None):
+        self._check_buffers(dA, dB, (out0, out1, out2))
         LB.check(LB.lib().msa_plan_run(self._h, _ptr(dA), _ptr(dB), _ptr(out0), _ptr(out1), _ptr(out2),
                                        _stream_ptr(stream)), "msa_plan_run")
 
     def results(self, stream=None):
+        """Per-pair results; raises MsaError(TIMEOUT) if any run since creation / clear_error() had a kernel
+        wait hit its spin limit (the plan's error word is sticky)."""
         n = len(self.ms)
         arr = (LB.PairResult * n)()
         LB.check(LB.lib().msa_plan_results(self._h, arr, _stream_ptr(stream)), "msa_plan_results")
         return [dict(score=r.score, status=r.status, end=(r.end_i, r.end_j), fin=tuple(r.fin)) for r in arr]
+
+    def error(self, stream=None) -> int:
+        """The sticky error word (0 = every run since creation / clear_error() completed its waits)."""
+        v = C.c_int()
+        LB.check(LB.lib().msa_plan_error(self._h, C.byref(v), _stream_ptr(stream)), "msa_plan_error")
+        return int(v.value)
+
+    def clear_error(self, stream=None) -> None:
+        LB.check(LB.lib().msa_plan_clear_error(self._h, _stream_ptr(stream)), "msa_plan_clear_error")
+
+    def scores_into(self, d_scores, stream=None) -> None:
+        """Copy the last run's per-pair scores into a device int32 tensor (stream-ordered, no host sync)."""
+        import torch
+
+        if not d_scores.is_cuda or d_scores.dtype != torch.int32 or not d_scores.is_contiguous() or \
+                d_scores.numel() < len(self.ms):
+            raise ValueError("d_scores must be a contiguous int32 CUDA tensor of n_pairs elements")
+        LB.check(LB.lib().msa_plan_scores(self._h, _ptr(d_scores), _stream_ptr(stream)), "msa_plan_scores")
 
     def stripe_meta(self, stream=None) -> np.ndarray:
         out = np.zeros((self.n_stripes, META_FIELDS), dtype=np.int32)

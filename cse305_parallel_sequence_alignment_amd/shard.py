@@ -2,17 +2,21 @@
 
 The hot path has no cross-pair dependency: a batch of pairs (C4: 1024 pairs of
 4,000 x 4,000) is split into contiguous blocks, one per rank, and every rank
-fills its block with its own stripe kernel launch.  The only collective is the
-tiny score all-gather at the end (RCCL over xGMI on MI355X, gloo in the CPU
-tests) -- there is no data-path exchange, so scaling is weak.
+fills its block with its own kernel launch.  The only collectives are the
+broadcast of the shared reference sequence (once) and the score all-gather at
+the end of every step (RCCL over xGMI on MI355X, gloo in the CPU tests) --
+there is no data-path exchange, so scaling is weak.
 
-This mirrors how the reference parallelises *across* subproblems
-(main_alignment.cpp:389-401: independent Subproblem objects handed to threads)
-one level up: pairs -> ranks instead of subproblems -> threads.
+This mirrors how the reference parallelises *across* pairs
+(testing.cpp:112-158: one std::thread per pair, each calling
+main_alignment_function) one level up: pairs -> ranks instead of pairs ->
+threads.  ``bench.py`` (workload c4) and ``tests/test_dist_gloo.py`` drive the
+same ``ShardedBatch``; only the per-rank scorer differs (a device Plan vs the
+CPU oracle).
 """
 from __future__ import annotations
 
-from typing import Callable, List, Sequence, Tuple
+from typing import Callable, Tuple
 
 
 def shard_range(n_units: int, rank: int, world: int) -> Tuple[int, int]:
@@ -24,8 +28,17 @@ def shard_range(n_units: int, rank: int, world: int) -> Tuple[int, int]:
     return lo, min(n_units, lo + per)
 
 
+def broadcast_reference(ref, src: int = 0, group=None):
+    """Every rank gets rank ``src``'s reference-sequence codes (in place; no-op at world size 1)."""
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.broadcast(ref, src=src, group=group)
+    return ref
+
+
 def gather_scores(local, n_units: int, rank: int, world: int, group=None):
-    """All-gather every rank's int64 score block into the full ``n_units`` vector (same device as ``local``)."""
+    """All-gather every rank's score block into the full ``n_units`` int64 vector (on ``local``'s device)."""
     import torch
     import torch.distributed as dist
 
@@ -42,14 +55,19 @@ def gather_scores(local, n_units: int, rank: int, world: int, group=None):
     return torch.cat(parts)[:n_units]
 
 
-def sharded_scores(pairs: Sequence, scorer: Callable[[Sequence], List[int]], rank: int, world: int, device="cpu",
-                   group=None):
-    """Score ``pairs`` across ranks: rank r runs ``scorer`` on its block, then all ranks get every score.
+class ShardedBatch:
+    """``n_units`` independent pairs split over ``world`` ranks.
 
-    ``scorer`` is the per-rank compute (on a GPU box: a ``Plan`` over the block's
-    pairs, see bench.py workload c4)."""
-    import torch
+    ``score_block(lo, hi)`` computes the scores of pairs [lo, hi) on this rank
+    and returns them as an integer tensor (device-resident on a GPU box: a Plan
+    built once for the block, run, then ``Plan.scores_into``).  ``step()`` runs
+    it and all-gathers every rank's scores."""
 
-    lo, hi = shard_range(len(pairs), rank, world)
-    mine = torch.tensor(list(scorer(pairs[lo:hi])) if hi > lo else [], dtype=torch.int64, device=device)
-    return gather_scores(mine, len(pairs), rank, world, group=group)
+    def __init__(self, n_units: int, rank: int, world: int, score_block: Callable, group=None):
+        self.n_units, self.rank, self.world, self.group = n_units, rank, world, group
+        self.lo, self.hi = shard_range(n_units, rank, world)
+        self.score_block = score_block
+
+    def step(self):
+        local = self.score_block(self.lo, self.hi)
+        return gather_scores(local, self.n_units, self.rank, self.world, group=self.group)

@@ -146,8 +146,19 @@ int msa_plan_cells_size(const msa_plan* plan, int64_t* elems);
  * (H: cells0; DIR: cells0 as uint8; TAB: three planes), may be NULL for NONE. */
 int msa_plan_run(msa_plan* plan, const uint8_t* dA, const uint8_t* dB, void* cells0, void* cells1, void* cells2,
                  void* stream);
-/* Copy per-pair results to the host (synchronizes `stream`). */
+/* Copy per-pair results to the host (synchronizes `stream`).  Returns
+ * MSA_ERR_TIMEOUT if any run since the plan was created (or since the last
+ * msa_plan_clear_error) had a kernel wait hit its spin limit: the plan's error
+ * word is sticky, so one check after many runs covers all of them. */
 int msa_plan_results(msa_plan* plan, msa_pair_result* out, void* stream);
+/* The sticky error word (0 = no error; else the kernel site code), synchronizes. */
+int msa_plan_error(msa_plan* plan, int* code, void* stream);
+/* Reset the sticky error word (stream-ordered). */
+int msa_plan_clear_error(msa_plan* plan, void* stream);
+/* Per-pair scores of the last run into a device int32 array of n_pairs
+ * (device-to-device copy on `stream`, no host sync): the input of a score
+ * all-gather across ranks. */
+int msa_plan_scores(msa_plan* plan, int32_t* d_scores, void* stream);
 /* Per-stripe metadata (cs, phases ...) of the last run: 12 int32 per stripe. */
 int msa_plan_stripe_meta(msa_plan* plan, int32_t* out, int64_t cap_stripes, void* stream);
 int64_t msa_plan_stripes(const msa_plan* plan);
@@ -158,7 +169,7 @@ int64_t msa_plan_stripes(const msa_plan* plan);
  * row rho = (i-1)%R, step t = j - cs_s + r lives at element
  * out_off + ((s*pmax*4 + t/4)*R + rho)*256 + r*4 + t%4 (DIR bytes, R = 1:
  * (s*pmax + t/16)*1024 + r*16 + t%16), cs_s = meta[12*(stripe0+s)].  R = 2 only
- * for two-pass single-pair SW-linear H plans (MSA_R=2). */
+ * for two-pass single-pair SW-linear H plans. */
 int msa_plan_pair_layout(const msa_plan* plan, int64_t pair, int64_t* out4);
 /* Order-independent digest of pair `pair`'s H cells (oracle orc_checksum_h). */
 int msa_plan_checksum(msa_plan* plan, const int32_t* dH, int64_t pair, uint64_t* digest, void* stream);

@@ -464,8 +464,13 @@ int orc_sw(const char* A, const char* B, uint64_t m, uint64_t n, int32_t match, 
  * max(T1,T2,T3) as int32 for in-band interior cells and 0 elsewhere.
  * Uses O(n) memory per table row pair.
  * ------------------------------------------------------------------------- */
-int orc_banded_ref(const char* A, const char* B, uint64_t m, uint64_t n, uint64_t w, double g, double h,
-                   int32_t* Hout, double* score) {
+static inline uint64_t splitmix64(uint64_t x);
+uint64_t orc_mix(uint64_t i, uint64_t j);
+
+/* digest (optional): orc_checksum_h(H, m, n, n+1, w) of the in-band H cells,
+ * accumulated on the fly (C3's 97k x 97k H does not fit in host memory). */
+int orc_banded_ref2(const char* A, const char* B, uint64_t m, uint64_t n, uint64_t w, double g, double h,
+                    int32_t* Hout, double* score, uint64_t* digest) {
   if ((m > n ? m - n : n - m) > w) return ORC_ERR_ARG;
   const double NI = -INFINITY;
   const uint64_t W = n + 1;
@@ -475,8 +480,13 @@ int orc_banded_ref(const char* A, const char* B, uint64_t m, uint64_t n, uint64_
   p1[0] = 0; p2[0] = NI; p3[0] = NI;
   for (uint64_t j = 1; j <= n; j++) { p1[j] = NI; p3[j] = NI; p2[j] = (j <= w) ? -h - g * (double)j : NI; }
   if (Hout) memset(Hout, 0, sizeof(int32_t) * (m + 1) * W);
+  for (uint64_t j = 0; j <= n; j++) { c1[j] = NI; c2[j] = NI; c3[j] = NI; }
+  uint64_t acc = 0;
   for (uint64_t i = 1; i <= m; i++) {
-    for (uint64_t j = 0; j <= n; j++) { c1[j] = NI; c2[j] = NI; c3[j] = NI; }
+    /* c holds row i-2 (band [i-2-w, i-2+w]): -inf over that and row i's band and their rims */
+    const uint64_t rlo = (i > w + 3) ? i - w - 3 : 0;
+    const uint64_t rhi = (i + w + 1 < n) ? i + w + 1 : n;
+    for (uint64_t j = rlo; j <= rhi; j++) { c1[j] = NI; c2[j] = NI; c3[j] = NI; }
     if (i <= w) c3[0] = -h - g * (double)i;
     const uint64_t jlo = (i > w) ? i - w : 1;
     const uint64_t jhi = (i + w < n) ? i + w : n;
@@ -485,7 +495,9 @@ int orc_banded_ref(const char* A, const char* B, uint64_t m, uint64_t n, uint64_
       c1[j] = f + dmax(dmax(p1[j - 1], p2[j - 1]), p3[j - 1]);
       c3[j] = dmax(dmax(p1[j] - g - h, p2[j] - g - h), p3[j] - g);
       c2[j] = dmax(dmax(c1[j - 1] - g - h, c2[j - 1] - g), c3[j - 1] - g - h);
-      if (Hout) Hout[i * W + j] = (int32_t)dmax(dmax(c1[j], c2[j]), c3[j]);
+      const int32_t hv = (int32_t)dmax(dmax(c1[j], c2[j]), c3[j]);
+      if (Hout) Hout[i * W + j] = hv;
+      if (digest) acc += orc_mix(i, j) * (uint64_t)(uint32_t)hv;
     }
     double* t;
     t = p1; p1 = c1; c1 = t;
@@ -493,8 +505,14 @@ int orc_banded_ref(const char* A, const char* B, uint64_t m, uint64_t n, uint64_
     t = p3; p3 = c3; c3 = t;
   }
   *score = dmax(dmax(p1[n], p2[n]), p3[n]);
+  if (digest) *digest = acc;
   free(p1); free(p2); free(p3); free(c1); free(c2); free(c3);
   return ORC_OK;
+}
+
+int orc_banded_ref(const char* A, const char* B, uint64_t m, uint64_t n, uint64_t w, double g, double h,
+                   int32_t* Hout, double* score) {
+  return orc_banded_ref2(A, B, m, n, w, g, h, Hout, score, NULL);
 }
 
 /* ---------------------------------------------------------------------------

@@ -5,6 +5,8 @@ leg, always as the checker (never as the measured or shipped path).
 
 * ``liboracle.so``: the C restatement in ``msa_oracle.c`` (each function cites
   the reference file:line it follows).
+* ``librowsweep.so``: the reference's CPU *method* (row sweep, fresh std::threads
+  per phase, prefix-max T2) restated in ``cpu_rowsweep.cpp`` -- the CPU baseline.
 * ``_ref/libref_sub.so`` / ``_ref/libref_partial.so``: the reference's own
   ``subproblem_alignment.cpp`` / ``partial.cpp`` compiled unmodified from
   /root/reference (``oracle/Makefile``); present only where they were built.
@@ -56,6 +58,7 @@ def lib():
         L.orc_partial_partition.argtypes = [P, P, P, P, P, P, u64, u64, u64, C.c_double, P, u64, P]
         L.orc_sw.argtypes = [P, P, u64, u64, C.c_int32, C.c_int32, C.c_int32, C.c_int32, P, P, P, P, P, P, P, u64]
         L.orc_banded_ref.argtypes = [P, P, u64, u64, u64, C.c_double, C.c_double, P, P]
+        L.orc_banded_ref2.argtypes = [P, P, u64, u64, u64, C.c_double, C.c_double, P, P, P]
         L.orc_checksum_h.argtypes = [P, u64, u64, u64, C.c_int64]
         L.orc_checksum_h.restype = C.c_uint64
         L.orc_mix.argtypes = [u64, u64]
@@ -173,14 +176,18 @@ def sw(A: bytes, B: bytes, match=1, mismatch=0, gap_open=1, gap_extend=1, want_h
     return r
 
 
-def banded_ref(A: bytes, B: bytes, w: int, g=1.0, h=2.0, want_h=False):
+def banded_ref(A: bytes, B: bytes, w: int, g=1.0, h=2.0, want_h=False, want_digest=False):
+    """Banded reference Gotoh: score [, H] [, in-band H digest = checksum_h(H, w) without materialising H]."""
     a, b = _bytes0(A), _bytes0(B)
     m, n = len(A), len(B)
     H = np.empty((m + 1, n + 1), dtype=np.int32) if want_h else None
     sc = C.c_double(0)
-    rc = lib().orc_banded_ref(_ptr(a), _ptr(b), m, n, w, g, h, _ptr(H), C.byref(sc))
+    dg = C.c_uint64(0)
+    rc = lib().orc_banded_ref2(_ptr(a), _ptr(b), m, n, w, g, h, _ptr(H), C.byref(sc),
+                               C.byref(dg) if want_digest else None)
     assert rc == 0, rc
-    return (sc.value, H) if want_h else sc.value
+    out = [sc.value] + ([H] if want_h else []) + ([int(dg.value)] if want_digest else [])
+    return out[0] if len(out) == 1 else tuple(out)
 
 
 def checksum_h(H: np.ndarray, w: int = -1) -> int:
@@ -202,6 +209,31 @@ def mix_matrix(m: int, n: int) -> np.ndarray:
     return x | np.uint64(1)
 
 
+_rowsweep = None
+
+
+def rowsweep(A: bytes, B: bytes, p: int = 1, mode: int = 1, g=1.0, h=2.0, match=1, mismatch=0, rows=0):
+    """The reference's CPU method (cpu_rowsweep.cpp): row sweep with p' fresh threads per phase.
+
+    mode 0 = the reference's global Gotoh (double), mode 1 = SW linear int32 (C2/C4).
+    Fills rows 1..rows (0 = all); returns (score, seconds)."""
+    global _rowsweep
+    if _rowsweep is None:
+        path = HERE / "librowsweep.so"
+        if not path.exists():
+            build()
+        L = C.CDLL(str(path))
+        L.cpu_rowsweep.argtypes = [C.c_int, C.c_char_p, C.c_char_p, C.c_size_t, C.c_size_t, C.c_size_t, C.c_double,
+                                   C.c_double, C.c_int, C.c_int, C.c_size_t, C.POINTER(C.c_double),
+                                   C.POINTER(C.c_double)]
+        _rowsweep = L
+    sc, secs = C.c_double(), C.c_double()
+    rc = _rowsweep.cpu_rowsweep(mode, A, B, len(A), len(B), p, g, h, match, mismatch, rows, C.byref(sc),
+                                C.byref(secs))
+    assert rc == 0, rc
+    return sc.value, secs.value
+
+
 # ----------------------------------------------------------------------------
 # The reference's own code (oracle/_ref) -- only where it was built.
 # ----------------------------------------------------------------------------
@@ -217,7 +249,7 @@ def ref_sub():
         P = C.c_void_p
         s = C.c_size_t
         L.ref_subproblem.argtypes = [P, P, s, s, s, s, s, C.c_int, C.c_int, C.c_double, C.c_double, P, P, P, P, s,
-                                     P, P, P, P, P, P]
+                                     P, P, P, P, P, P, P, P]
         _ref_sub = L
     return _ref_sub
 
@@ -235,8 +267,11 @@ def ref_partial_lib():
 
 
 def ref_subproblem(A: bytes, B: bytes, start_type=-1, end_type=-1, g=1.0, h=2.0, p=1, idA=0, idB=0, m=None,
-                   n=None, tables=True, traceback=True):
-    """Run the reference's own Subproblem (compute_tables + find_alignment)."""
+                   n=None, tables=True, traceback=True, digest=False):
+    """Run the reference's own Subproblem (compute_tables + find_alignment).
+
+    Always returns the final cell ``fin`` = (T1, T2, T3)[m'][n']; ``digest`` adds
+    ``h_digest`` = checksum_h of H = max(T1, T2, T3) computed inside the driver."""
     a, b = _bytes1(A), _bytes1(B)
     m = len(A) - idA if m is None else m
     n = len(B) - idB if n is None else n
@@ -250,10 +285,14 @@ def ref_subproblem(A: bytes, B: bytes, start_type=-1, end_type=-1, g=1.0, h=2.0,
     inv = C.c_int(0)
     nn_ = C.c_size_t(0)
     secs = C.c_double(0)
+    fin = np.zeros(3, dtype=np.float64)
+    dg = C.c_uint64(0)
     ref_sub().ref_subproblem(_ptr(a), _ptr(b), m, n, idA, idB, p, start_type, end_type, g, h, _ptr(T[0]),
                              _ptr(T[1]), _ptr(T[2]), C.byref(inv), cap, C.byref(nn_), _ptr(ni), _ptr(nj), _ptr(nt),
-                             _ptr(endn), C.byref(secs))
-    r = dict(invert=bool(inv.value), T1=T[0], T2=T[1], T3=T[2], fill_seconds=secs.value)
+                             _ptr(endn), C.byref(secs), _ptr(fin), C.byref(dg) if digest else None)
+    r = dict(invert=bool(inv.value), T1=T[0], T2=T[1], T3=T[2], fill_seconds=secs.value, fin=tuple(fin.tolist()))
+    if digest:
+        r["h_digest"] = int(dg.value)
     if traceback:
         k = nn_.value
         r["nodes"] = [(int(ni[q]), int(nj[q]), int(nt[q])) for q in range(k)]

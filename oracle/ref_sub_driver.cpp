@@ -8,6 +8,7 @@
 // main_alignment.cpp does not compile as shipped (wrong include at
 // main_alignment.cpp:6-7, conflict marker at :405), so it is NOT built; its
 // single-subproblem glue is restated in msa_oracle.c:orc_main_alignment.
+#include <algorithm>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -23,13 +24,33 @@ extern "C" {
 int ref_subproblem(const char* A, const char* B, size_t m, size_t n, size_t idA, size_t idB, size_t p,
                    int start_type, int end_type, double g, double h, double* T1, double* T2, double* T3,
                    int* invert, size_t nodes_cap, size_t* n_nodes, unsigned long long* nodes_i,
-                   unsigned long long* nodes_j, int* nodes_t, unsigned long long* end_node, double* fill_seconds) {
+                   unsigned long long* nodes_j, int* nodes_t, unsigned long long* end_node, double* fill_seconds,
+                   double* fin3, unsigned long long* h_digest) {
   Subproblem sp(const_cast<char*>(A), const_cast<char*>(B), m, n, idA, idB, p, start_type, end_type, g, h);
   auto t0 = std::chrono::steady_clock::now();
   sp.compute_tables();
   auto t1 = std::chrono::steady_clock::now();
   if (fill_seconds) *fill_seconds = std::chrono::duration<double>(t1 - t0).count();
   *invert = sp.invert ? 1 : 0;
+  if (fin3) {  // the tables' final cell (m', n')
+    fin3[0] = sp.T1[sp.m][sp.n];
+    fin3[1] = sp.T2[sp.m][sp.n];
+    fin3[2] = sp.T3[sp.m][sp.n];
+  }
+  if (h_digest) {  // oracle orc_checksum_h of H = max(T1,T2,T3) over rows/columns >= 1
+    unsigned long long acc = 0;
+    for (size_t i = 1; i <= sp.m; i++)
+      for (size_t j = 1; j <= sp.n; j++) {
+        const double hv = std::max(std::max(sp.T1[i][j], sp.T2[i][j]), sp.T3[i][j]);
+        unsigned long long x = ((unsigned long long)i << 32) | j;
+        x += 0x9E3779B97F4A7C15ull;
+        x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+        x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+        x = (x ^ (x >> 31)) | 1ull;
+        acc += x * (unsigned long long)(unsigned)(int)hv;
+      }
+    *h_digest = acc;
+  }
   if (T1) {
     const size_t W = sp.n + 1;
     for (size_t i = 0; i <= sp.m; i++) {

@@ -5,13 +5,15 @@ unmodified subproblem_alignment.cpp / partial.cpp compiled by oracle/Makefile.
 The fixtures written here are data (inputs + expected outputs) and are
 committed; the GPU box never needs /root/reference.
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py            # small fixtures
+    python tests/golden/make_golden.py at_size    # 10k / 20k fixtures (at_size.json)
 
 Outputs (tests/golden/):
   kat.json             known-answer tests + harness-pair outputs
   subproblem_tables.npz  full T1/T2/T3 for small random pairs, every start/end type
   subproblem_paths.json  find_alignment node lists for the same + dataset prefixes
   partial.json         findPartialBalancedPartitionParallel partitions (wrap semantics)
+  at_size.json         scores / node lists / H digests at 10k and 20k (reference p'=1)
 """
 from __future__ import annotations
 
@@ -48,6 +50,30 @@ def print_seq_lines(A: bytes, B: bytes, nodes):
     l1 = "".join(chr(a[i]) if t in (1, 3) else "-" for i, j, t in nodes)
     l2 = "".join(chr(b[j]) if t in (1, 2) else "-" for i, j, t in nodes)
     return l1, l2
+
+
+def at_size():
+    """Reference-produced fixtures at C2/C5 sizes: the reference's own
+    Subproblem (p'=1) on seq0 x seq1 at 10k and 20k, seq0 x seq5 at 20k and h = 0 at 10k: score,
+    final cell, node count, md5 of print_seq's two lines, and the H digest (checksum_h of
+    max(T1,T2,T3)) where the fixture says so.  Writes tests/golden/at_size.json."""
+    if not O.ref_available():
+        O.build()
+    assert O.ref_available(), "oracle/_ref not built (needs /root/reference)"
+    _, seqs = O.load_dataset()
+    out = []
+    for (ia, ib, L, g, h, dig) in [(0, 1, 10000, 1.0, 2.0, True), (0, 1, 10000, 1.0, 0.0, False),
+                                   (0, 1, 20000, 1.0, 2.0, True), (0, 5, 20000, 1.0, 2.0, False)]:
+        A, B = seqs[ia][:L], seqs[ib][:L]
+        r = O.ref_subproblem(A, B, -1, -1, g, h, p=1, tables=False, digest=dig)
+        l1, l2 = print_seq_lines(A, B, r["nodes"])
+        d = dict(a=ia, b=ib, L=L, g=g, h=h, score=float(max(r["fin"])), fin=list(r["fin"]),
+                 n_nodes=len(r["nodes"]), lines_md5=hashlib.md5((l1 + "\n" + l2 + "\n").encode()).hexdigest())
+        if dig:
+            d["h_checksum"] = str(r["h_digest"])
+        out.append(d)
+        print("at_size", ia, ib, L, h, d["score"], flush=True)
+    (HERE / "at_size.json").write_text(json.dumps(out, indent=1))
 
 
 def main():
@@ -144,4 +170,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["at_size"]:
+        at_size()
+    else:
+        main()

@@ -1,8 +1,9 @@
 """World-size-2 sharding path on CPU (gloo): pairs split over ranks, scores all-gathered.
 
-The per-rank compute on a GPU box is the stripe kernel; here each rank scores
-its block with the oracle so the sharding/gather logic (shard.py, used by
-bench.py's multi-GPU c4 workload) is checked without a GPU."""
+bench.py's multi-GPU c4 workload runs ``shard.ShardedBatch`` with a device Plan
+as the per-rank scorer; here the same class runs with the oracle as the
+scorer, so the split, the reference broadcast and the gather are checked
+without a GPU."""
 import os
 import socket
 
@@ -25,22 +26,28 @@ def _worker(rank, world, port, n_pairs, q):
     sys.path.insert(0, str(ROOT))
     import torch.distributed as dist
 
-    from cse305_parallel_sequence_alignment_amd.shard import shard_range, sharded_scores
+    import torch
+
+    from cse305_parallel_sequence_alignment_amd.shard import ShardedBatch, broadcast_reference, shard_range
     from oracle import oracle as O
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         rng = np.random.default_rng(42)
-        pairs = [(rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), 50 + 7 * k).tobytes(),
-                  rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), 60).tobytes()) for k in range(n_pairs)]
+        queries = [rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), 50 + 7 * k).tobytes() for k in range(n_pairs)]
+        # only rank 0 holds the reference sequence; the broadcast gives it to every rank
+        ref = torch.from_numpy(np.frombuffer(b"ACGT" * 15, dtype=np.uint8).copy()) if rank == 0 else \
+            torch.zeros(60, dtype=torch.uint8)
+        ref = bytes(broadcast_reference(ref).numpy())
         seen = []
 
-        def scorer(block):
-            seen.extend(block)
-            return [O.sw(a, b, 2, -1, 1, 1)["score"] for a, b in block]
+        def score_block(lo, hi):
+            seen.extend(range(lo, hi))
+            return torch.tensor([O.sw(queries[k], ref, 2, -1, 1, 1)["score"] for k in range(lo, hi)],
+                                dtype=torch.int32)
 
-        got = sharded_scores(pairs, scorer, rank, world)
+        got = ShardedBatch(n_pairs, rank, world, score_block).step()
         lo, hi = shard_range(n_pairs, rank, world)
         q.put((rank, got.tolist(), len(seen), hi - lo))
     finally:
@@ -63,9 +70,8 @@ def test_sharded_scores_world2(n_pairs):
         p.join(timeout=60)
         assert p.exitcode == 0
     rng = np.random.default_rng(42)
-    pairs = [(rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), 50 + 7 * k).tobytes(),
-              rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), 60).tobytes()) for k in range(n_pairs)]
-    want = [O.sw(a, b, 2, -1, 1, 1)["score"] for a, b in pairs]
+    queries = [rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), 50 + 7 * k).tobytes() for k in range(n_pairs)]
+    want = [O.sw(a, b"ACGT" * 15, 2, -1, 1, 1)["score"] for a in queries]
     for rank, got, nseen, nblock in out:
         assert got == want
         assert nseen == nblock

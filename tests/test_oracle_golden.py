@@ -96,3 +96,65 @@ def test_restatement_vs_reference_live(oracle):
         assert [tuple(x) for x in r["nodes"]] == [tuple(x) for x in ref["nodes"]]
         p = int(rng.integers(1, 6))
         assert oracle.partial_partition(A, B, p, 1.0, 2.0, 1, 1) == oracle.ref_partial(A, B, p, 1.0, 2.0, 1, 1)
+
+
+def test_oracle_at_size_10k(oracle, dataset):
+    """The C restatement reproduces the reference's own 10k outputs (at_size.json: score, node count, md5 of the
+    print_seq lines) for g=1 with h=2 and h=0."""
+    _, seqs = dataset
+    for c in json.loads((GOLDEN / "at_size.json").read_text()):
+        if c["L"] != 10000:
+            continue
+        A, B = seqs[c["a"]][:c["L"]], seqs[c["b"]][:c["L"]]
+        text, score = oracle.main_alignment_text(A, B, c["g"], c["h"])
+        lines = text.split("\n")[5:7]
+        assert score == c["score"] and len(lines[0]) == c["n_nodes"]
+        assert hashlib.md5((lines[0] + "\n" + lines[1] + "\n").encode()).hexdigest() == c["lines_md5"]
+
+
+def test_at_size_scores_are_the_surveyed_ones():
+    """at_size.json holds the reference scores SURVEY.md §8(c) probed: 8094 / 8112 (h=0) / 18049 / 6522."""
+    got = {(c["a"], c["b"], c["L"], c["h"]): c["score"] for c in json.loads((GOLDEN / "at_size.json").read_text())}
+    assert got == {(0, 1, 10000, 2.0): 8094.0, (0, 1, 10000, 0.0): 8112.0, (0, 1, 20000, 2.0): 18049.0,
+                   (0, 5, 20000, 2.0): 6522.0}
+
+
+@pytest.mark.parametrize("p", [1, 3, 8])
+def test_rowsweep_baseline_matches_oracle(oracle, dataset, p):
+    """The CPU baseline (the reference's row-sweep method, oracle/cpu_rowsweep.cpp) computes the same scores as
+    the oracle: the reference's Gotoh (mode 0) and C2's SW-linear (mode 1), at several thread counts."""
+    _, seqs = dataset
+    A, B = seqs[0][:1500], seqs[1][:1400]
+    s0, _ = oracle.rowsweep(A, B, p=p, mode=0, g=1.0, h=2.0)
+    assert s0 == oracle.main_alignment_text(A, B, 1.0, 2.0)[1]
+    s1, _ = oracle.rowsweep(A, B, p=p, mode=1, g=1.0, match=1, mismatch=0)
+    assert s1 == oracle.sw(A, B, 1, 0, 1, 1)["score"]
+
+
+def test_banded_digest_equals_checksum(oracle):
+    rng = np.random.default_rng(9)
+    A = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), 900).tobytes()
+    B = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), 880).tobytes()
+    for w in (20, 64, 1000):
+        s, H, d = oracle.banded_ref(A, B, w, 1.0, 2.0, want_h=True, want_digest=True)
+        assert d == oracle.checksum_h(H, w)
+
+
+def test_c4_fixture_sample(oracle):
+    """A sample of the committed C4 scores (make_c4_scores.py, all 1024 made by the oracle) re-computed."""
+    from cse305_parallel_sequence_alignment_amd import data
+
+    fx = json.loads((GOLDEN / "c4_scores.json").read_text())
+    assert len(fx["scores"]) == data.C4_PAIRS
+    ref = data.c4_reference()
+    for k in (0, 1, 511, 1023):
+        assert oracle.sw(data.c4_queries(k, k + 1)[0], ref, 1, 0, 1, 1)["score"] == fx["scores"][k]
+
+
+def test_fasta_reader_matches_oracle_loader(dataset):
+    """data.read_and_store_sequences (pull_data.cpp:18-71) reads the bundled file like the oracle's loader."""
+    from cse305_parallel_sequence_alignment_amd import data
+
+    names, seqs = data.read_and_store_sequences()
+    assert (names and len(names) == len(seqs) == 20)
+    assert [n.decode() for n in names] == dataset[0] and seqs == dataset[1]
