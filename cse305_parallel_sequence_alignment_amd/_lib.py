@@ -80,6 +80,16 @@ def lib() -> C.CDLL:
     L.msa_partial_partition.argtypes = [P, P, sz, sz, sz, C.c_double, C.c_double, C.c_int, C.c_int, P, sz,
                                         C.POINTER(sz)]
     L.msa_partial_tables.argtypes = [P, P, sz, sz, C.c_double, C.c_double, C.c_int, C.c_int, P, P, P, P, P, P]
+    L.msa_non_parallel_tables.argtypes = [P, P, sz, sz, sz, sz, C.c_int, C.c_int, C.c_double, C.c_double, P, sz,
+                                          C.POINTER(sz)]
+    L.msa_subproblem_f64.argtypes = [P, P, sz, sz, sz, sz, C.c_int, C.c_double, C.c_double, C.c_int, P, P, P,
+                                     C.POINTER(C.c_int)]
+    L.msa_subproblem_row.argtypes = [C.c_int, P, P, sz, sz, sz, sz, C.c_int, C.c_double, C.c_double, sz, sz, P, P,
+                                     P, P, P, P, P]
+    L.msa_optimal_alignment.argtypes = [P, P, sz, sz, sz, C.c_double, C.c_double, P, sz, C.c_int, P, sz,
+                                        C.POINTER(sz), P, sz, C.POINTER(sz)]
+    L.msa_main_alignment_partitioned.argtypes = [P, P, sz, sz, sz, C.c_double, C.c_double, C.c_int, P, sz,
+                                                 C.POINTER(sz)]
     L.msa_plan_create.argtypes = [C.POINTER(PlanDesc), C.POINTER(P)]
     L.msa_plan_destroy.argtypes = [P]
     L.msa_plan_destroy.restype = None
@@ -116,6 +126,8 @@ class _Bind:
 # Every symbol include/msa.h declares (checked by the CPU test suite).
 EXPORTED = [
     "msa_status_string", "msa_version", "msa_device_count", "msa_main_alignment", "msa_subproblem",
+    "msa_non_parallel_tables", "msa_optimal_alignment", "msa_main_alignment_partitioned",
+    "msa_subproblem_f64", "msa_subproblem_row",
     "msa_partial_partition", "msa_partial_tables", "msa_plan_create", "msa_plan_destroy", "msa_plan_cells_size",
     "msa_plan_run", "msa_plan_results", "msa_plan_error", "msa_plan_clear_error", "msa_plan_scores",
     "msa_plan_stripe_meta", "msa_plan_stripes", "msa_plan_pair_layout",

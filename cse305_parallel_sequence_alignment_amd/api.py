@@ -6,6 +6,7 @@ library or GPU raises ``MsaError`` / ``ImportError``).
 
 Reference interfaces mirrored (D-2n/CSE305_Parallel_Sequence_Alignment):
   main_alignment_function   alignment_algorithm/main_alignment.h:38, .cpp:353-410
+  optimal_alignment         main_alignment.h:34, .cpp:158-351 (multi-subproblem stitch)
   Subproblem                alignment_algorithm/subproblem_alignment.h:16-97
   Align                     subproblem_alignment.h:8-13 (``align``)
   findPartialBalancedPartitionParallel  sequence_alignment/partial.h:41, partial.cpp:149-163
@@ -131,13 +132,23 @@ class Subproblem:
         conv = lambda t: np.where(t == np.iinfo(np.int32).min, -np.inf, t.astype(np.float64))
         self.T1, self.T2, self.T3 = (conv(t) for t in T)
 
+    def non_parallel_tables_text(self) -> str:
+        """The text subproblem_alignment.cpp:401-421 prints, from the GPU tables (msa_non_parallel_tables)."""
+        A, B, m, n, ida, idb = self._orig
+        L = LB.lib()
+        need = C.c_size_t()
+        LB.check(L.msa_non_parallel_tables(A, B, m, n, ida, idb, self.start_type, self.end_type, self.g, self.h,
+                                           None, 0, C.byref(need)), "msa_non_parallel_tables")
+        buf = C.create_string_buffer(need.value + 1)
+        LB.check(L.msa_non_parallel_tables(A, B, m, n, ida, idb, self.start_type, self.end_type, self.g, self.h,
+                                           buf, need.value + 1, C.byref(need)), "msa_non_parallel_tables")
+        return buf.raw[:need.value].decode("latin-1")
+
     def non_parallel_tables(self) -> None:
-        """subproblem_alignment.cpp:357-422: same tables, then prints them as the reference does."""
+        """subproblem_alignment.cpp:357-422: the same tables (GPU fill), printed as the reference does."""
         self.compute_tables()
-        for name, t in (("T1", self.T1), ("T2", self.T2), ("T3", self.T3)):
-            print(f"{name}:")
-            for row in t:
-                print("".join(f"{v:f} " for v in row))
+        sys.stdout.write(self.non_parallel_tables_text())
+        sys.stdout.flush()
 
     def find_alignment(self) -> None:
         """subproblem_alignment.cpp:105-172 (tie order, quirks Q1/Q2 included)."""
@@ -158,6 +169,63 @@ class Subproblem:
         """subproblem_alignment.cpp:174-180."""
         for (i, j, t) in self.alignment_list():
             print(f"({i}, {j}, {t})")
+
+
+def _nodes_in(partial_bp):
+    arr = (LB.Node * max(1, len(partial_bp)))()
+    for k, a in enumerate(partial_bp):
+        i, j, t = a.as_tuple() if isinstance(a, Align) else a
+        arr[k].i, arr[k].j, arr[k].t = i, j, t
+    return arr
+
+
+def optimal_alignment_text(A, B, partial_bp, m, n, p=32, g=1.0, h=2.0, fix_all=False):
+    """``optimal_alignment`` (main_alignment.cpp:202-351) over the partition ``partial_bp``
+    (Align nodes or (i, j, t) tuples): returns (stdout text, stitched path as (i, j, t) tuples).
+
+    fix_all=False keeps the reference's behaviour (2-3 subproblems: only the first is
+    solved; the link into the last subproblem is never made, :344-348)."""
+    A, B = _buf(A), _buf(B)
+    if len(A) < m + 1 or len(B) < n + 1:
+        raise ValueError("A/B must be 1-based buffers of at least m+1 / n+1 bytes")
+    L = LB.lib()
+    bp = _nodes_in(partial_bp)
+    fl = 1 if fix_all else 0
+    need, npath = C.c_size_t(), C.c_size_t()
+    cap = m + n + 2 * len(partial_bp) + 2
+    path = (LB.Node * cap)()
+    LB.check(L.msa_optimal_alignment(A, B, m, n, p, g, h, bp, len(partial_bp), fl, None, 0, C.byref(need), path,
+                                     cap, C.byref(npath)), "msa_optimal_alignment")
+    buf = C.create_string_buffer(need.value + 1)
+    LB.check(L.msa_optimal_alignment(A, B, m, n, p, g, h, bp, len(partial_bp), fl, buf, need.value + 1,
+                                     C.byref(need), None, 0, None), "msa_optimal_alignment")
+    nodes = [(int(path[k].i), int(path[k].j), int(path[k].t)) for k in range(npath.value)]
+    return buf.raw[:need.value].decode("latin-1"), nodes
+
+
+def optimal_alignment(A, B, partial_bp, m, n, p, g, h) -> None:
+    """Drop-in for ``void optimal_alignment(char*, char*, std::vector<align>, size_t m, size_t n,
+    size_t p, double g, double h)``: prints what the reference prints."""
+    text, _ = optimal_alignment_text(A, B, partial_bp, m, n, p, g, h)
+    sys.stdout.write(text)
+    sys.stdout.flush()
+
+
+def main_alignment_partitioned_text(A, B, m, n, p=4, g=1.0, h=2.0, fix_all=False) -> str:
+    """main_alignment_function with its commented-out partition step enabled
+    (main_alignment.cpp:365,372): GPU partition -> optimal_alignment."""
+    A, B = _buf(A), _buf(B)
+    if len(A) < m + 1 or len(B) < n + 1:
+        raise ValueError("A/B must be 1-based buffers of at least m+1 / n+1 bytes")
+    L = LB.lib()
+    need = C.c_size_t()
+    fl = 1 if fix_all else 0
+    LB.check(L.msa_main_alignment_partitioned(A, B, m, n, p, g, h, fl, None, 0, C.byref(need)),
+             "msa_main_alignment_partitioned")
+    buf = C.create_string_buffer(need.value + 1)
+    LB.check(L.msa_main_alignment_partitioned(A, B, m, n, p, g, h, fl, buf, need.value + 1, C.byref(need)),
+             "msa_main_alignment_partitioned")
+    return buf.raw[:need.value].decode("latin-1")
 
 
 def print_seq(A: bytes, B: bytes, begin: Optional[Align]) -> str:

@@ -13,12 +13,14 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <map>
 #include <vector>
 
 #include "../../include/msa.h"
 #include "msa_kernels.hip"
 #include "msa_flow.hip"
+#include "msa_rowsweep.hip"
 
 using namespace msa;
 
@@ -54,6 +56,104 @@ int ensure_device() {
     }
   }
   return g_dev_ok ? MSA_OK : MSA_ERR_NODEV;
+}
+
+// Device memory pool.  The reference's harness calls main_alignment_function
+// from hardware_concurrency threads at once (testing.cpp:145-158, 269-280,
+// 352-358); with plain hipMalloc/hipFree every call would serialize on
+// hipFree's implicit device synchronization.  Blocks are cached per size class
+// (powers of two up to 1 MiB, then 2 MiB multiples) in one mutex-protected
+// free list; a block is only returned by its owner after the stream work that
+// used it has completed (run_one syncs its stream, msa_plan_destroy syncs the
+// plan's last stream), so a block never changes hands while a kernel uses it.
+class DevPool {
+ public:
+  static size_t size_class(size_t b) {
+    if (b < 256) b = 256;
+    if (b <= (size_t(1) << 20)) {
+      size_t c = 256;
+      while (c < b) c <<= 1;
+      return c;
+    }
+    const size_t mb2 = size_t(2) << 20;
+    return (b + mb2 - 1) / mb2 * mb2;
+  }
+  void* get(size_t bytes) {
+    const size_t c = size_class(bytes);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      auto it = free_.find(c);
+      if (it != free_.end()) {
+        void* p = it->second;
+        free_.erase(it);
+        cached_ -= c;
+        return p;
+      }
+    }
+    void* p = nullptr;
+    if (hipMalloc(&p, c) != hipSuccess) return nullptr;
+    return p;
+  }
+  void put(void* p, size_t bytes) {
+    if (!p) return;
+    const size_t c = size_class(bytes);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (cached_ + c <= kCap) {
+        free_.emplace(c, p);
+        cached_ += c;
+        return;
+      }
+    }
+    (void)hipFree(p);
+  }
+  size_t cached() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return cached_;
+  }
+
+ private:
+  static constexpr size_t kCap = size_t(8) << 30;  // bytes kept cached (HBM is 288 GB)
+  std::mutex mu_;
+  std::multimap<size_t, void*> free_;
+  size_t cached_ = 0;
+};
+
+DevPool& dev_pool() {
+  static DevPool* p = new DevPool();  // never destroyed: no HIP calls during static teardown
+  return *p;
+}
+
+// Non-blocking streams reused across calls (creating one costs ~10s of us).
+class StreamPool {
+ public:
+  hipStream_t get() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (!free_.empty()) {
+        hipStream_t s = free_.back();
+        free_.pop_back();
+        return s;
+      }
+    }
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    return s;
+  }
+  void put(hipStream_t s) {
+    if (!s) return;
+    std::lock_guard<std::mutex> lk(mu_);
+    free_.push_back(s);
+  }
+
+ private:
+  std::mutex mu_;
+  std::vector<hipStream_t> free_;
+};
+
+StreamPool& stream_pool() {
+  static StreamPool* p = new StreamPool();
+  return *p;
 }
 
 int nc_of(int alg) {
@@ -167,6 +267,19 @@ struct msa_plan {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   uint32_t epoch = 0;
   unsigned long long* stamps = nullptr;  // diagnostic build
+  hipStream_t last_stream = nullptr;     // stream of the last run (msa_plan_destroy waits on it)
+  bool ran = false;
+  std::vector<std::pair<void*, size_t>> blocks;  // pooled device blocks owned by the plan
+
+  // a pooled device block of `bytes`, owned by the plan
+  template <class T>
+  bool alloc(T** p, size_t bytes) {
+    void* q = dev_pool().get(bytes);
+    if (!q) return false;
+    blocks.emplace_back(q, bytes);
+    *p = (T*)q;
+    return true;
+  }
 };
 
 extern "C" {
@@ -401,27 +514,27 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   }
   // device buffers
   auto fail = [&](void) { msa_plan_destroy(P); return MSA_ERR_HIP; };
-  if (hipMalloc(&P->d_pairs, sizeof(msa_pair_desc) * P->pairs.size()) != hipSuccess) return fail();
+  if (!P->alloc(&P->d_pairs, sizeof(msa_pair_desc) * P->pairs.size())) return fail();
   if (hipMemcpy(P->d_pairs, P->pairs.data(), sizeof(msa_pair_desc) * P->pairs.size(), hipMemcpyHostToDevice) !=
       hipSuccess)
     return fail();
-  if (hipMalloc(&P->d_meta, sizeof(msa_stripe_meta) * std::max<int64_t>(1, P->total_stripes)) != hipSuccess)
+  if (!P->alloc(&P->d_meta, sizeof(msa_stripe_meta) * std::max<int64_t>(1, P->total_stripes)))
     return fail();
   if (hipMemset(P->d_meta, 0, sizeof(msa_stripe_meta) * std::max<int64_t>(1, P->total_stripes)) != hipSuccess)
     return fail();
-  if (hipMalloc(&P->d_ticket, 64) != hipSuccess) return fail();
-  if (hipMalloc(&P->d_err, 64) != hipSuccess || hipMemset(P->d_err, 0, 64) != hipSuccess) return fail();
-  if (hipMalloc(&P->d_cod, (size_t)MSA_NCOPY * P->cod_copy + 64) != hipSuccess) return fail();
-  if (hipMalloc(&P->d_segs, sizeof(msa_pair_desc) * P->segs.size()) != hipSuccess) return fail();
+  if (!P->alloc(&P->d_ticket, 64)) return fail();
+  if (!P->alloc(&P->d_err, 64) || hipMemset(P->d_err, 0, 64) != hipSuccess) return fail();
+  if (!P->alloc(&P->d_cod, (size_t)MSA_NCOPY * P->cod_copy + 64)) return fail();
+  if (!P->alloc(&P->d_segs, sizeof(msa_pair_desc) * P->segs.size())) return fail();
   if (hipMemcpy(P->d_segs, P->segs.data(), sizeof(msa_pair_desc) * P->segs.size(), hipMemcpyHostToDevice) !=
       hipSuccess)
     return fail();
-  if (hipMalloc(&P->d_res, sizeof(PairResult) * desc->n_pairs) != hipSuccess) return fail();
-  if (hipMalloc(&P->d_sum, 64) != hipSuccess) return fail();
+  if (!P->alloc(&P->d_res, sizeof(PairResult) * desc->n_pairs)) return fail();
+  if (!P->alloc(&P->d_sum, 64)) return fail();
   if (single && kp.n_items > 1) {
     P->gbuf_stride = (int)(((desc->n[0] + 2 * MSA_GOFF + 16) + 15) & ~15);
     const size_t gb = (size_t)(kp.n_items - 1) * P->nc * P->gbuf_stride * sizeof(unsigned long long);
-    if (hipMalloc(&P->d_gbuf, gb) != hipSuccess) return fail();
+    if (!P->alloc(&P->d_gbuf, gb)) return fail();
     if (hipMemset(P->d_gbuf, 0, gb) != hipSuccess) return fail();
   }
   if (P->flow2) {
@@ -440,10 +553,10 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return key[x] < key[y]; });
     const size_t brb = sizeof(unsigned long long) * (size_t)S * P->brw;
     const size_t snb = sizeof(unsigned long long) * (size_t)P->nblk * 128 * P->R;
-    if (hipMalloc(&P->d_br, brb) != hipSuccess || hipMemset(P->d_br, 0, brb) != hipSuccess) return fail();
-    if (hipMalloc(&P->d_snap, snb) != hipSuccess || hipMemset(P->d_snap, 0, snb) != hipSuccess) return fail();
-    if (hipMalloc(&P->d_blk, sizeof(int4) * (size_t)P->nblk) != hipSuccess) return fail();
-    if (hipMalloc(&P->d_order, sizeof(int) * (size_t)P->nblk) != hipSuccess) return fail();
+    if (!P->alloc(&P->d_br, brb) || hipMemset(P->d_br, 0, brb) != hipSuccess) return fail();
+    if (!P->alloc(&P->d_snap, snb) || hipMemset(P->d_snap, 0, snb) != hipSuccess) return fail();
+    if (!P->alloc(&P->d_blk, sizeof(int4) * (size_t)P->nblk)) return fail();
+    if (!P->alloc(&P->d_order, sizeof(int) * (size_t)P->nblk)) return fail();
     if (hipMemcpy(P->d_order, order.data(), sizeof(int) * (size_t)P->nblk, hipMemcpyHostToDevice) != hipSuccess)
       return fail();
   }
@@ -454,19 +567,9 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
 
 void msa_plan_destroy(msa_plan* P) {
   if (!P) return;
-  if (P->d_pairs) (void)hipFree(P->d_pairs);
-  if (P->d_meta) (void)hipFree(P->d_meta);
-  if (P->d_ticket) (void)hipFree(P->d_ticket);
-  if (P->d_err) (void)hipFree(P->d_err);
-  if (P->d_gbuf) (void)hipFree(P->d_gbuf);
-  if (P->d_cod) (void)hipFree(P->d_cod);
-  if (P->d_segs) (void)hipFree(P->d_segs);
-  if (P->d_res) (void)hipFree(P->d_res);
-  if (P->d_sum) (void)hipFree(P->d_sum);
-  if (P->d_br) (void)hipFree(P->d_br);
-  if (P->d_snap) (void)hipFree(P->d_snap);
-  if (P->d_blk) (void)hipFree(P->d_blk);
-  if (P->d_order) (void)hipFree(P->d_order);
+  // the plan's blocks go back to the pool: its last run must be complete
+  if (P->ran) (void)hipStreamSynchronize(P->last_stream);
+  for (auto& b : P->blocks) dev_pool().put(b.first, b.second);
   if (P->ev0) (void)hipEventDestroy(P->ev0);
   if (P->ev1) (void)hipEventDestroy(P->ev1);
   delete P;
@@ -495,6 +598,8 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
   if (P->d.cells != MSA_CELLS_NONE && !c0) return MSA_ERR_ARG;
   if (P->d.cells == MSA_CELLS_TAB && (!c1 || !c2)) return MSA_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
+  P->last_stream = st;
+  P->ran = true;
   KArgs a;
   std::memset(&a, 0, sizeof(a));
   a.kp = P->kp;
@@ -627,3 +732,4 @@ int msa_plan_checksum(msa_plan* P, const int32_t* dH, int64_t pair, uint64_t* di
 
 }  // extern "C"
 #include "msa_refapi.inc"
+#include "msa_rowapi.inc"

@@ -17,6 +17,12 @@
  *                        subproblem_alignment.cpp:329-355 (fill), :105-172 (traceback)
  *   msa_partial_partition findPartialBalancedPartitionParallel(...)
  *                        sequence_alignment/partial.h:41, partial.cpp:149-163
+ *   msa_non_parallel_tables  Subproblem::non_parallel_tables(), subproblem_alignment.cpp:357-422
+ *   msa_subproblem_f64   Subproblem ctor + compute_tables() in double for any g, h (:251-355)
+ *   msa_subproblem_row   Subproblem::compute_row / *MapThread bodies (:212-327)
+ *   msa_optimal_alignment optimal_alignment(...), main_alignment.h:34, main_alignment.cpp:158-351
+ *   msa_main_alignment_partitioned  main_alignment_function with its commented-out
+ *                        partition step (main_alignment.cpp:365,372) enabled
  *   msa_partial_tables   initializeTables/initializeReverseTables/fillTablesParallel/
  *                        fillReverseTablesParallel, partial.h:25-35, partial.cpp:13-79
  *   msa_plan_*           device-resident batch / single-pair fills (build extension:
@@ -82,6 +88,69 @@ int msa_main_alignment(const char* A1, const char* B1, size_t m, size_t n, size_
 int msa_subproblem(const char* A1, const char* B1, size_t m, size_t n, size_t idA, size_t idB, int start_type,
                    int end_type, double g, double h, int32_t* T1, int32_t* T2, int32_t* T3, msa_node* nodes,
                    size_t nodes_cap, size_t* n_nodes, msa_node* end_node, int* invert);
+
+/* Subproblem::non_parallel_tables (subproblem_alignment.cpp:357-422): the
+ * tables of msa_subproblem printed as the reference prints them ("T1:" then
+ * one line per row of "%lf " cells, -inf as "-inf"; then T2, T3) into `text`
+ * (NUL-terminated; *text_len = its length; text may be NULL to size it). */
+int msa_non_parallel_tables(const char* A1, const char* B1, size_t m, size_t n, size_t idA, size_t idB,
+                            int start_type, int end_type, double g, double h, char* text, size_t text_cap,
+                            size_t* text_len);
+
+/* The reference's tables in IEEE double for ANY g, h (the int32 entry points
+ * need integral g, h): Subproblem ctor + compute_tables
+ * (subproblem_alignment.h:36-74, .cpp:329-355) as its row sweep -- T1/T3
+ * elementwise, T2 by omega + inclusive prefix max (:229-326) -- on the GPU,
+ * with the same double operations in the same order (bit-identical cells).
+ * T1/T2/T3: (m'+1) x (n'+1) row-major doubles (-inf as -infinity), m' =
+ * min(m,n) after the constructor's swap (*invert).  m = n = 0 is MSA_ERR_ARG.
+ * mode MSA_F64_NON_PARALLEL computes T2 by non_parallel_tables' direct
+ * recurrence (:398) instead -- the same values for integral g, h; for others
+ * the two forms round differently, and each mode matches its reference twin. */
+enum { MSA_F64_COMPUTE_TABLES = 0, MSA_F64_NON_PARALLEL = 1 };
+int msa_subproblem_f64(const char* A1, const char* B1, size_t m, size_t n, size_t idA, size_t idB, int start_type,
+                       double g, double h, int mode, double* T1, double* T2, double* T3, int* invert);
+
+/* One step of the reference's row sweep on the GPU (double, bit-identical),
+ * for the source-compatible Subproblem's compute_row and MapThread bodies:
+ *   MSA_ROW_ZERO  compute_row(0)                  subproblem_alignment.cpp:259-280 (cur = row 0)
+ *   MSA_ROW_FULL  compute_row(i > 0)              :282-326 (up = row i-1, cur = row i; vec optional)
+ *   MSA_ROW_FIRST ComputeFirstRowMapThread         :212-227 on cur, columns [start, end)
+ *   MSA_ROW_13    ComputeRowMapThread13            :229-235 up -> cur T1/T3, columns [start, end)
+ *   MSA_ROW_OMEGA ComputeOmegaMapThread            :237-242 cur T1/T3 -> vec[start, end)
+ *   MSA_ROW_T2    ComputeRowMapThread2             :244-249 vec -> cur T2, columns [start, end)
+ * A1/B1 with idA/idB as the Subproblem holds them (after its swap); rows are
+ * n+1 doubles; column ranges need 1 <= start <= end <= n+1. */
+enum { MSA_ROW_FIRST = 1, MSA_ROW_13 = 2, MSA_ROW_OMEGA = 4, MSA_ROW_T2 = 8, MSA_ROW_ZERO = 16, MSA_ROW_FULL = 32 };
+int msa_subproblem_row(int part, const char* A1, const char* B1, size_t idA, size_t idB, size_t n, size_t i,
+                       int start_type, double g, double h, size_t start, size_t end, const double* up1,
+                       const double* up2, const double* up3, double* cur1, double* cur2, double* cur3, double* vec);
+
+/* optimal_alignment(A, B, partial_bp, m, n, p, g, h) (main_alignment.h:34,
+ * main_alignment.cpp:202-351): solves the subproblems between consecutive
+ * partition points bp[k] -> bp[k+1] (start type bp[k].t, end type -bp[k+1].t)
+ * on the GPU, concurrently, in the reference's selection (with 2 or 3
+ * subproblems only subproblem 0 is solved, :237-279), stitches their node
+ * lists as :344-348 does (the link into the last subproblem is never made) and
+ * writes the stdout text: "bp1".."bp4" per solved subproblem, then print_seq's
+ * two lines.  flags = MSA_OPT_FIX_ALL solves and links every subproblem.
+ * path (may be NULL) receives the stitched node list.  p only sizes the
+ * reference's thread counts (omega / ParallelPrefix / assign_processors,
+ * :158-200) and is accepted for signature parity.  Partition points must be
+ * non-decreasing in i and j and inside [0,m] x [0,n]; a 0 x 0 subproblem is
+ * MSA_ERR_ARG (the reference crashes on both). */
+enum { MSA_OPT_FIX_ALL = 1 };
+int msa_optimal_alignment(const char* A1, const char* B1, size_t m, size_t n, size_t p, double g, double h,
+                          const msa_node* bp, size_t n_bp, int flags, char* text, size_t text_cap, size_t* text_len,
+                          msa_node* path, size_t path_cap, size_t* n_path);
+
+/* main_alignment_function with the partition step the reference leaves
+ * commented out (main_alignment.cpp:365,372): the GPU partition
+ * findPartialBalancedPartitionParallel(A1+1, B1+1, m, n, p, g, h, -1, -1)
+ * (partial.cpp reads A[i-1], so it gets the 0-based view) feeding
+ * msa_optimal_alignment.  Same text contract as msa_main_alignment. */
+int msa_main_alignment_partitioned(const char* A1, const char* B1, size_t m, size_t n, size_t p, double g,
+                                   double h, int flags, char* text, size_t text_cap, size_t* text_len);
 
 /* findPartialBalancedPartitionParallel (partial.cpp:149-163), int32 wrap
  * semantics; A0/B0 are 0-based (partial.cpp reads A[i-1]).  out receives the

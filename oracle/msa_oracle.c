@@ -21,6 +21,9 @@
  *   orc_print_seq          main_alignment.cpp:32-55
  *   orc_main_alignment     main_alignment.cpp:11-22 (OptimalAlignmentMapThread),
  *                          :202-351 (single-subproblem path), :353-410
+ *   orc_optimal_alignment  main_alignment.cpp:202-351 (subproblem selection of the
+ *                          three rounds :232-341, stitch :344-348 incl. the
+ *                          never-made link into the last subproblem), :32-55
  *   orc_partial_tables / orc_partial_partition
  *                          partial.cpp:9-163 with two's-complement wrap (the
  *                          reference's -O0 behaviour)
@@ -235,6 +238,90 @@ int64_t orc_main_alignment(const char* A, const char* B, uint64_t m, uint64_t n,
   memcpy(out + o, l2, len); o += len; out[o++] = '\n';
   out[o] = 0;
   free(l1); free(l2); free(nodes);
+  return (int64_t)o;
+}
+
+/* optimal_alignment(A, B, partial_bp, m, n, p, g, h), main_alignment.cpp:202-351,
+ * over the partition bp[0..nbp).  Subproblem k = Subproblem(A, B, bp[k+1].i -
+ * bp[k].i, bp[k+1].j - bp[k].j, bp[k].i, bp[k].j, p', bp[k].t, -bp[k+1].t, g, h)
+ * (:239-253).  Selection (:232-341): round r = 0,1,2 takes r, r+3, ... while
+ * i < num-3 and then the first i past that if i < num; rounds 1-2 only run when
+ * num > 3.  Stitch (:344-348): end of k-1 -> begin of k for k = 1..num-2 (the
+ * last subproblem is never linked; fix_all links and solves everything).  The
+ * walk from pointers[0] stops at an unsolved subproblem or an empty one
+ * (alignment_begin == NULL).  Output: "bp1".."bp4" per solved subproblem, then
+ * print_seq (:32-55).  *n_path receives the stitched path (path may be NULL).
+ * Returns bytes of text written, or < 0. */
+int64_t orc_optimal_alignment(const char* A, const char* B, uint64_t m, uint64_t n, const orc_node* bp,
+                              uint64_t nbp, double g, double h, int fix_all, char* out, uint64_t cap,
+                              orc_node* path, uint64_t path_cap, uint64_t* n_path) {
+  if (nbp < 2) return ORC_ERR_ARG;
+  const uint64_t num = nbp - 1;
+  for (uint64_t k = 0; k < num; k++) {
+    if (bp[k + 1].i < bp[k].i || bp[k + 1].j < bp[k].j || bp[k + 1].i > m || bp[k + 1].j > n) return ORC_ERR_ARG;
+    if (bp[k + 1].i == bp[k].i && bp[k + 1].j == bp[k].j) return ORC_ERR_ARG;
+  }
+  char* solved = (char*)calloc(num, 1);
+  uint64_t n_solved = 0;
+  if (fix_all) {
+    for (uint64_t k = 0; k < num; k++) solved[k] = 1;
+  } else {
+    const int num_sub_3 = num > 3;
+    for (uint64_t r = 0; r < 3; r++) {
+      if (r > 0 && !num_sub_3) break;
+      uint64_t i = r;
+      while (num_sub_3 && i < num - 3) { solved[i] = 1; i += 3; }
+      if (i < num) solved[i] = 1;
+    }
+  }
+  for (uint64_t k = 0; k < num; k++) n_solved += solved[k];
+  orc_node* acc = (orc_node*)malloc(sizeof(orc_node) * (m + n + 2 * nbp + 2));
+  uint64_t L = 0;
+  const uint64_t last_link = fix_all ? num - 1 : (num >= 2 ? num - 2 : 0);
+  int rc = ORC_OK;
+  for (uint64_t k = 0; k < num; k++) {
+    if (!solved[k]) break;
+    const uint64_t lenA = bp[k + 1].i - bp[k].i, lenB = bp[k + 1].j - bp[k].j;
+    const uint64_t idA = bp[k].i, idB = bp[k].j;
+    const uint64_t mm = lenA <= lenB ? lenA : lenB, nn = lenA <= lenB ? lenB : lenA;
+    double* T1 = (double*)malloc(sizeof(double) * (mm + 1) * (nn + 1));
+    double* T2 = (double*)malloc(sizeof(double) * (mm + 1) * (nn + 1));
+    double* T3 = (double*)malloc(sizeof(double) * (mm + 1) * (nn + 1));
+    orc_node* nodes = (orc_node*)malloc(sizeof(orc_node) * (lenA + lenB + 2));
+    int inv;
+    orc_subproblem_tables(A, B, lenA, lenB, idA, idB, bp[k].t, g, h, T1, T2, T3, &inv);
+    uint64_t len = 0;
+    orc_node endn;
+    rc = orc_subproblem_traceback(inv ? B : A, inv ? A : B, mm, nn, inv ? idB : idA, inv ? idA : idB,
+                                  -bp[k + 1].t, g, h, T1, T2, T3, nodes, lenA + lenB + 2, &len, &endn);
+    free(T1); free(T2); free(T3);
+    if (rc != ORC_OK) { free(nodes); break; }
+    memcpy(acc + L, nodes, sizeof(orc_node) * len);
+    L += len;
+    free(nodes);
+    if (len == 0) break;                           /* alignment_begin == NULL */
+    if (k + 1 > last_link || k + 1 >= num) break;  /* end node's next stays NULL */
+  }
+  /* subproblems past the walk are still solved by the reference (their bp lines print) */
+  free(solved);
+  if (rc != ORC_OK) { free(acc); return rc; }
+  if (n_path) *n_path = L;
+  if (path) {
+    if (L > path_cap) { free(acc); return ORC_ERR_CAP; }
+    memcpy(path, acc, sizeof(orc_node) * L);
+  }
+  const char* hdr = "bp1\nbp1.2\nbp2\nbp3\nbp4\n";
+  const uint64_t need = strlen(hdr) * n_solved + 2 * (L + 1) + 1;
+  if (need > cap) { free(acc); return ORC_ERR_CAP; }
+  uint64_t o = 0;
+  for (uint64_t k = 0; k < n_solved; k++) { memcpy(out + o, hdr, strlen(hdr)); o += strlen(hdr); }
+  char* l1 = (char*)malloc(L + 1);
+  char* l2 = (char*)malloc(L + 1);
+  orc_print_seq(A, B, m, n, acc, L, l1, l2);
+  memcpy(out + o, l1, L); o += L; out[o++] = '\n';
+  memcpy(out + o, l2, L); o += L; out[o++] = '\n';
+  out[o] = 0;
+  free(l1); free(l2); free(acc);
   return (int64_t)o;
 }
 

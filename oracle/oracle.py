@@ -54,6 +54,9 @@ def lib():
                                                P, u64, P, P]
         L.orc_main_alignment.argtypes = [P, P, u64, u64, C.c_double, C.c_double, P, u64, P]
         L.orc_main_alignment.restype = C.c_int64
+        L.orc_optimal_alignment.argtypes = [P, P, u64, u64, P, u64, C.c_double, C.c_double, C.c_int, P, u64, P,
+                                            u64, P]
+        L.orc_optimal_alignment.restype = C.c_int64
         L.orc_partial_tables.argtypes = [P, P, u64, u64, C.c_double, C.c_double, C.c_int, C.c_int, P, P, P, P, P, P]
         L.orc_partial_partition.argtypes = [P, P, P, P, P, P, u64, u64, u64, C.c_double, P, u64, P]
         L.orc_sw.argtypes = [P, P, u64, u64, C.c_int32, C.c_int32, C.c_int32, C.c_int32, P, P, P, P, P, P, P, u64]
@@ -132,6 +135,26 @@ def main_alignment_text(A: bytes, B: bytes, g=1.0, h=2.0):
     if rc < 0:
         raise RuntimeError(f"oracle main_alignment rc={rc}")
     return out[:rc].tobytes().decode("latin-1"), score.value
+
+
+def optimal_alignment(A: bytes, B: bytes, bp, g=1.0, h=2.0, fix_all=False):
+    """optimal_alignment (main_alignment.cpp:202-351) over partition bp [(i, j, t), ...] for
+    0-based python strings A, B (placed 1-based).  Returns (stdout text, stitched path)."""
+    a, b = _bytes1(A), _bytes1(B)
+    arr = np.zeros(len(bp), dtype=NODE_DT)
+    for k, (i, j, t) in enumerate(bp):
+        arr[k]["i"], arr[k]["j"], arr[k]["t"] = i, j, t
+    cap = 64 * len(bp) + 2 * (len(A) + len(B) + 4)
+    out = np.zeros(cap, dtype=np.uint8)
+    pcap = len(A) + len(B) + 2 * len(bp) + 2
+    path = np.zeros(pcap, dtype=NODE_DT)
+    npath = C.c_uint64(0)
+    rc = lib().orc_optimal_alignment(_ptr(a), _ptr(b), len(A), len(B), _ptr(arr), len(bp), g, h,
+                                     1 if fix_all else 0, _ptr(out), cap, _ptr(path), pcap, C.byref(npath))
+    if rc < 0:
+        raise RuntimeError(f"oracle optimal_alignment rc={rc}")
+    nodes = [(int(x["i"]), int(x["j"]), int(x["t"])) for x in path[:npath.value]]
+    return out[:rc].tobytes().decode("latin-1"), nodes
 
 
 def partial_tables(A: bytes, B: bytes, g=1.0, h=2.0, start_type=1, end_type=1):

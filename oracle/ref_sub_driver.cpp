@@ -11,7 +11,10 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
+#include <fcntl.h>
+#include <unistd.h>
 
 #include "subproblem_alignment.h"
 
@@ -81,6 +84,34 @@ int ref_subproblem(const char* A, const char* B, size_t m, size_t n, size_t idA,
       a = nx;
     }
     if (sp.alignment_begin == NULL) std::free(sp.alignment_end);
+  }
+  return 0;
+}
+
+// Runs Subproblem(...).non_parallel_tables() (subproblem_alignment.cpp:357-422:
+// the direct recurrence, then the tables printed to stdout).  The printed text
+// goes to text_path (stdout is redirected around the call); the tables are
+// copied out as in ref_subproblem.
+int ref_non_parallel(const char* A, const char* B, size_t m, size_t n, size_t idA, size_t idB, size_t p,
+                     int start_type, int end_type, double g, double h, double* T1, double* T2, double* T3,
+                     int* invert, const char* text_path) {
+  Subproblem sp(const_cast<char*>(A), const_cast<char*>(B), m, n, idA, idB, p, start_type, end_type, g, h);
+  std::fflush(stdout);
+  const int saved = dup(1);
+  const int fd = open(text_path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+  if (saved < 0 || fd < 0) return -1;
+  dup2(fd, 1);
+  close(fd);
+  sp.non_parallel_tables();
+  std::fflush(stdout);
+  dup2(saved, 1);
+  close(saved);
+  *invert = sp.invert ? 1 : 0;
+  const size_t W = sp.n + 1;
+  for (size_t i = 0; i <= sp.m; i++) {
+    std::memcpy(T1 + i * W, sp.T1[i].data(), sizeof(double) * W);
+    std::memcpy(T2 + i * W, sp.T2[i].data(), sizeof(double) * W);
+    std::memcpy(T3 + i * W, sp.T3[i].data(), sizeof(double) * W);
   }
   return 0;
 }

@@ -145,3 +145,23 @@ def test_compat_library_exports_reference_symbol():
     assert lib.exists(), "build libmsa_compat.so (make -C cse305_parallel_sequence_alignment_amd/csrc)"
     L = C.CDLL(str(lib))
     assert hasattr(L, "_Z23main_alignment_functionPcS_mmmdd")
+
+
+SUBPROBLEM_SYMBOLS = [
+    "_ZN10Subproblem14compute_tablesEv", "_ZN10Subproblem19non_parallel_tablesEv", "_ZN10Subproblem11compute_rowEm",
+    "_ZN10Subproblem14find_alignmentEv", "_ZN10Subproblem15print_alignmentEv",
+    "_ZN10Subproblem24ComputeFirstRowMapThreadEPS_mm", "_ZN10Subproblem21ComputeRowMapThread13EPS_mmm",
+    "_ZN10Subproblem21ComputeOmegaMapThreadEPS_mmmRSt6vectorIdSaIdEE",
+    "_ZN10Subproblem20ComputeRowMapThread2EPS_mmmRSt6vectorIdSaIdEE",
+]
+
+
+def test_compat_library_exports_subproblem_members():
+    """libmsa_compat.so defines every out-of-line member of the reference's class Subproblem
+    (alignment_algorithm/subproblem_alignment.h:76-95) with the reference's C++ mangling, and the
+    test driver built against include/subproblem_alignment_compat.h links."""
+    lib = ROOT / "cse305_parallel_sequence_alignment_amd" / "libmsa_compat.so"
+    L = C.CDLL(str(lib))
+    for sym in SUBPROBLEM_SYMBOLS:
+        assert hasattr(L, sym), sym
+    assert (ROOT / "tests" / "cpp" / "subproblem_driver").exists(), "make -C tests/cpp"

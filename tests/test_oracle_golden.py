@@ -158,3 +158,19 @@ def test_fasta_reader_matches_oracle_loader(dataset):
     names, seqs = data.read_and_store_sequences()
     assert (names and len(names) == len(seqs) == 20)
     assert [n.decode() for n in names] == dataset[0] and seqs == dataset[1]
+
+
+OPT = json.loads((GOLDEN / "optimal.json").read_text())
+
+
+@pytest.mark.parametrize("k", range(len(OPT)))
+def test_optimal_alignment_fixture(oracle, k):
+    """orc_optimal_alignment (main_alignment.cpp:202-351) against tests/golden/optimal.json: every
+    subproblem's nodes come from the reference's own Subproblem; reference selection + stitch and
+    the fixed (every subproblem linked) variant."""
+    c = OPT[k]
+    bp = [tuple(x) for x in c["bp"]]
+    for key, fix in (("ref", False), ("fix_all", True)):
+        text, path = oracle.optimal_alignment(c["A"].encode(), c["B"].encode(), bp, c["g"], c["h"], fix)
+        assert text == c[key]["text"]
+        assert [list(x) for x in path] == c[key]["path"]
