@@ -151,6 +151,8 @@ class StreamPool {
   std::vector<hipStream_t> free_;
 };
 
+std::atomic<uint32_t> g_epoch{0};  // granule epoch of the next run (msa_plan_run)
+
 StreamPool& stream_pool() {
   static StreamPool* p = new StreamPool();
   return *p;
@@ -561,6 +563,9 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
       return fail();
   }
   if (hipEventCreate(&P->ev0) != hipSuccess || hipEventCreate(&P->ev1) != hipSuccess) return fail();
+  // the memsets above went to the null stream, which does not order the non-blocking
+  // streams runs are launched on: finish them before the plan can run anywhere
+  if (hipStreamSynchronize(nullptr) != hipSuccess) return fail();
   *out = P;
   return MSA_OK;
 }
@@ -603,8 +608,12 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
   KArgs a;
   std::memset(&a, 0, sizeof(a));
   a.kp = P->kp;
-  if (++P->epoch == 0) P->epoch = 1;
-  a.kp.epoch = P->epoch;
+  // epochs are process-wide, so granules left in a pooled block by an earlier plan
+  // can never carry the epoch a new run polls for
+  uint32_t ep = g_epoch.fetch_add(1) + 1;
+  if (ep == 0) ep = g_epoch.fetch_add(1) + 1;
+  P->epoch = ep;
+  a.kp.epoch = ep;
   a.A = dA;
   a.B = dB;
   a.pairs = P->d_pairs;

@@ -6,8 +6,10 @@
 // (ComputeOmegaMapThread :237-242, omega[0] = T2[i][0]), an inclusive prefix
 // max (ParallelPrefixMax :13-103) and T2[i][j] = partial[j] - j*g
 // (ComputeRowMapThread2 :244-249).  This kernel performs exactly those double
-// operations in the same order (no FMA contraction: explicit _rn intrinsics;
-// max as std::max, (a < b) ? b : a), so every cell is bit-identical to the
+// operations in the same order (no FMA contraction: `fp contract(off)` below,
+// so every a*b and a+b rounds on its own as on the reference's x86 build; the
+// HIP __d*_rn intrinsics are plain operators that the default contraction mode
+// may fuse; max as std::max, (a < b) ? b : a), so every cell is bit-identical to the
 // reference for ANY g, h -- the int32 stripe kernels only take integral g, h.
 // The prefix max is order-independent, so the block scan below is exact.
 //
@@ -18,6 +20,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+
+#pragma clang fp contract(off)
 
 namespace msa {
 
@@ -32,6 +36,10 @@ enum RowPart : int {
 };
 
 __device__ __forceinline__ double rmax(double a, double b) { return (a < b) ? b : a; }  // std::max
+// one IEEE-rounded operation each (contraction is off in this file)
+__device__ __forceinline__ double dmul(double a, double b) { return a * b; }
+__device__ __forceinline__ double dadd(double a, double b) { return a + b; }
+__device__ __forceinline__ double dsub(double a, double b) { return a - b; }
 
 constexpr int RS_THREADS = 1024;
 
@@ -56,24 +64,24 @@ __device__ __forceinline__ void first_row_cell(const RowArgs& a, double* r1, dou
   const double NI = -__builtin_inf();
   r1[j] = NI;
   r3[j] = NI;
-  if (a.start_type == -2) r2[j] = __dmul_rn(-a.g, (double)j);
+  if (a.start_type == -2) r2[j] = dmul(-a.g, (double)j);
   else if (a.start_type == 1 || a.start_type == 3) r2[j] = NI;
-  else r2[j] = __dsub_rn(-a.h, __dmul_rn(a.g, (double)j));
+  else r2[j] = dsub(-a.h, dmul(a.g, (double)j));
 }
 
 __device__ __forceinline__ void cell13(const RowArgs& a, const double* u1, const double* u2, const double* u3,
                                        double* r1, double* r3, char ai, long long j) {
   const double f = (ai == a.B[j]) ? 1.0 : 0.0;
-  r1[j] = __dadd_rn(f, rmax(rmax(u1[j - 1], u2[j - 1]), u3[j - 1]));
-  const double gh1 = __dsub_rn(__dsub_rn(u1[j], a.g), a.h);
-  const double gh2 = __dsub_rn(__dsub_rn(u2[j], a.g), a.h);
-  r3[j] = rmax(rmax(gh1, gh2), __dsub_rn(u3[j], a.g));
+  r1[j] = dadd(f, rmax(rmax(u1[j - 1], u2[j - 1]), u3[j - 1]));
+  const double gh1 = dsub(dsub(u1[j], a.g), a.h);
+  const double gh2 = dsub(dsub(u2[j], a.g), a.h);
+  r3[j] = rmax(rmax(gh1, gh2), dsub(u3[j], a.g));
 }
 
 __device__ __forceinline__ double omega_of(const RowArgs& a, const double* r1, const double* r3, long long j) {
-  const double x = __dsub_rn(__dsub_rn(r1[j - 1], a.g), a.h);
-  const double y = __dsub_rn(__dsub_rn(r3[j - 1], a.g), a.h);
-  return __dadd_rn(__dmul_rn((double)j, a.g), rmax(x, y));
+  const double x = dsub(dsub(r1[j - 1], a.g), a.h);
+  const double y = dsub(dsub(r3[j - 1], a.g), a.h);
+  return dadd(dmul((double)j, a.g), rmax(x, y));
 }
 
 // inclusive prefix max of v[0..n] into out[0..n] (out may alias v)
@@ -132,7 +140,7 @@ __global__ __launch_bounds__(RS_THREADS) void rowsweep_kernel(RowArgs a) {
       for (long long j = a.start + t; j < a.end; j += RS_THREADS) a.vec[j] = omega_of(a, r1, r3, j);
     } else {
       for (long long j = a.start + t; j < a.end; j += RS_THREADS)
-        r2[j] = __dsub_rn(a.vec[j], __dmul_rn((double)j, a.g));
+        r2[j] = dsub(a.vec[j], dmul((double)j, a.g));
     }
     return;
   }
@@ -143,9 +151,9 @@ __global__ __launch_bounds__(RS_THREADS) void rowsweep_kernel(RowArgs a) {
     if (t == 0) {  // :282-292
       r1[0] = NI;
       r2[0] = NI;
-      if (a.start_type == -3) r3[0] = __dmul_rn(-a.g, (double)i);
+      if (a.start_type == -3) r3[0] = dmul(-a.g, (double)i);
       else if (a.start_type == 1 || a.start_type == 2) r3[0] = NI;
-      else r3[0] = __dsub_rn(-a.h, __dmul_rn(a.g, (double)i));
+      else r3[0] = dsub(-a.h, dmul(a.g, (double)i));
     }
     const char ai = a.A[i];
     for (long long j = 1 + t; j <= n; j += RS_THREADS) cell13(a, u1, u2, u3, r1, r3, ai, j);
@@ -157,9 +165,9 @@ __global__ __launch_bounds__(RS_THREADS) void rowsweep_kernel(RowArgs a) {
       if (t == 0) {
         double prev = r2[0];
         for (long long j = 1; j <= n; ++j) {
-          const double x = __dsub_rn(__dsub_rn(r1[j - 1], a.g), a.h);
-          const double y = __dsub_rn(prev, a.g);
-          const double z = __dsub_rn(__dsub_rn(r3[j - 1], a.g), a.h);
+          const double x = dsub(dsub(r1[j - 1], a.g), a.h);
+          const double y = dsub(prev, a.g);
+          const double z = dsub(dsub(r3[j - 1], a.g), a.h);
           prev = rmax(rmax(x, y), z);
           r2[j] = prev;
         }
@@ -172,7 +180,7 @@ __global__ __launch_bounds__(RS_THREADS) void rowsweep_kernel(RowArgs a) {
     __syncthreads();
     block_prefix_max(a.vec, a.vec, n, lds);
     __syncthreads();
-    for (long long j = 1 + t; j <= n; j += RS_THREADS) r2[j] = __dsub_rn(a.vec[j], __dmul_rn((double)j, a.g));
+    for (long long j = 1 + t; j <= n; j += RS_THREADS) r2[j] = dsub(a.vec[j], dmul((double)j, a.g));
     __syncthreads();
   }
 }
