@@ -15,7 +15,9 @@ one batch of input already resident in HBM:
 * c4: 1024 pairs of 4,000 x 4,000 SW (score only), sharded over ranks
   (shard.ShardedBatch); every step ends with an RCCL all-gather of the scores.
 * c3: one 97,403 x 97,403 banded (|i-j| <= 512) reference-Gotoh fill, H written.
-* c5: one 20k x 20k affine SW fill writing 1 B/cell traceback bits.
+* c5: one 20k x 20k affine SW fill writing 1 B/cell traceback bits, then the
+  traceback on the device (one wave walks the bits from the end cell): a step
+  is fill + traceback.
 
 After the timed steps (outside the timed region) the run is checked: the
 plan's sticky error word must be 0 (every timed step completed its waits), the
@@ -137,7 +139,8 @@ def main():
         plan_kw = dict(alg=LB.SW_AFFINE, cells=LB.CELLS_DIR, match=1, mismatch=0, gap_open=3, gap_extend=1,
                        track_end=True)
         cells_per_step = m * n
-        desc = "sw-affine 20000x20000, open 3 extend 1, 1 B/cell traceback bits written"
+        desc = ("sw-affine 20000x20000, open 3 extend 1, 1 B/cell traceback bits written + traceback on the "
+                "device (ops + begin cell)")
     else:  # c4
         total = data.C4_PAIRS
         L = data.C4_LEN
@@ -175,6 +178,13 @@ def main():
 
         def step():
             return batch.step()  # fill this rank's pairs, then RCCL all-gather of every rank's scores
+    elif wl == "c5":
+        tb_ops = torch.empty(m + n + 2, dtype=torch.uint8, device=dev)
+        tb_info = torch.zeros(4, dtype=torch.int64, device=dev)
+
+        def step():
+            plan.run(dA, dB, out)
+            plan.traceback_async(out, tb_ops, tb_info)  # same stream: walks the bits this run wrote
     else:
         def step():
             plan.run(dA, dB, out)
@@ -214,8 +224,15 @@ def main():
             checks["h_matches_cpu"] = bool(plan.checksum(out) == O.checksum_h(o["H"]))
             del o
     elif wl == "c5":
-        o = O.sw(A, B, 1, 0, 3, 1)
+        from cse305_parallel_sequence_alignment_amd.plan import cigar_of
+
+        o = O.sw(A, B, 1, 0, 3, 1, want_tb=(rank == 0))
         checks["score_matches_cpu"] = bool(o["score"] == res[0]["score"] and tuple(o["end"]) == tuple(res[0]["end"]))
+        if rank == 0:
+            inf = tb_info.cpu().tolist()
+            cig = cigar_of(bytes(tb_ops[:inf[0]].cpu().numpy().tobytes()))
+            checks["traceback_matches_cpu"] = bool(inf[3] == 0 and cig == o["cigar"] and
+                                                   (inf[1], inf[2]) == tuple(o["beg"]))
     elif wl == "c3":
         checks["score_matches_cpu"] = bool(int(O.banded_ref(A, B, 512, 1.0, 2.0)) == res[0]["score"])
     else:
@@ -236,6 +253,15 @@ def main():
         plan.run(dA, dB, out)
         kms.append(plan.kernel_ms())
     kern_ms = float(np.mean(kms))
+    tb_ms = None
+    if wl == "c5":  # the device traceback alone (torch events: it runs on torch's current stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            plan.traceback_async(out, tb_ops, tb_info)
+        e1.record()
+        torch.cuda.synchronize()
+        tb_ms = e0.elapsed_time(e1) / 5
     if plan.error():
         raise SystemExit(f"rank {rank}: a kernel wait hit its spin limit in the timing pass")
 
@@ -283,7 +309,8 @@ def main():
                                         f"dp{world} (one independent pair per GPU; RCCL bcast of the reference "
                                         f"once; no collective in the step)"),
                            score_rank0=int(res[0]["score"]), checks_all_ranks=bool(ok.item()), **checks,
-                           kernel_errors=0, dp_kernel_ms=round(kern_ms, 4)),
+                           kernel_errors=0, dp_kernel_ms=round(kern_ms, 4),
+                           **({"traceback_ms": round(tb_ms, 4)} if tb_ms is not None else {})),
             "roofline": roof,
             "cpu_baseline": cpu,
         }

@@ -21,6 +21,7 @@
 #include "msa_kernels.hip"
 #include "msa_flow.hip"
 #include "msa_rowsweep.hip"
+#include "msa_traceback.hip"
 
 using namespace msa;
 
@@ -724,6 +725,17 @@ int msa_plan_stripe_meta(msa_plan* P, int32_t* out, int64_t cap, void* stream) {
   static_assert(sizeof(msa_stripe_meta) == 12 * 4, "meta layout");
   HIPCHK(hipMemcpyAsync(out, P->d_meta, sizeof(msa_stripe_meta) * P->total_stripes, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  return MSA_OK;
+}
+
+int msa_plan_traceback(msa_plan* P, int64_t pair, const uint8_t* dDir, uint8_t* d_ops, int64_t ops_cap,
+                       int64_t* d_info, void* stream) {
+  if (!P || !dDir || !d_ops || !d_info || ops_cap < 0 || pair < 0 || pair >= P->d.n_pairs) return MSA_ERR_ARG;
+  if (P->kp.alg != MSA_ALG_SWA || P->d.cells != MSA_CELLS_DIR) return MSA_ERR_UNSUPPORTED;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(sw_traceback_kernel, dim3(1), dim3(64), 0, st, dDir, P->d_pairs, P->d_meta,
+                     (const PairResult*)P->d_res, (int)pair, d_ops, (long long)ops_cap, (long long*)d_info);
+  HIPCHK(hipGetLastError());
   return MSA_OK;
 }
 

@@ -151,6 +151,33 @@ class Plan:
                  "msa_plan_checksum")
         return int(v.value)
 
+    def traceback_async(self, dDir, d_ops, d_info, pair=0, stream=None) -> None:
+        """Device traceback (msa_plan_traceback) of an SW-affine DIR plan, stream-ordered after run():
+        d_ops (uint8, >= m+n) receives the ops end -> start, d_info (int64[4]) {n_ops, beg_i, beg_j, status}."""
+        import torch
+
+        if not (dDir.is_cuda and dDir.dtype == torch.uint8 and dDir.numel() >= self.cells_elems):
+            raise ValueError("dDir must be the uint8 CUDA tensor the plan's run() wrote")
+        if not (d_ops.is_cuda and d_ops.dtype == torch.uint8 and d_ops.is_contiguous()):
+            raise ValueError("d_ops must be a contiguous uint8 CUDA tensor")
+        if not (d_info.is_cuda and d_info.dtype == torch.int64 and d_info.numel() >= 4):
+            raise ValueError("d_info must be an int64 CUDA tensor of >= 4 elements")
+        LB.check(LB.lib().msa_plan_traceback(self._h, pair, _ptr(dDir), _ptr(d_ops), d_ops.numel(), _ptr(d_info),
+                                             _stream_ptr(stream)), "msa_plan_traceback")
+
+    def traceback(self, dDir, pair=0, stream=None):
+        """Device traceback, fetched: dict(ops=bytes end -> start, beg=(i, j), cigar=run-length string)."""
+        import torch
+
+        dev = dDir.device
+        ops = torch.empty(self.ms[pair] + self.ns[pair] + 2, dtype=torch.uint8, device=dev)
+        info = torch.zeros(4, dtype=torch.int64, device=dev)
+        self.traceback_async(dDir, ops, info, pair, stream)
+        inf = info.cpu().tolist()
+        LB.check(int(inf[3]), "msa_plan_traceback")
+        o = bytes(ops[:inf[0]].cpu().numpy().tobytes())
+        return dict(ops=o, beg=(int(inf[1]), int(inf[2])), cigar=cigar_of(o))
+
     def set_timing(self, on: bool) -> None:
         """Record HIP events around the DP kernel in run() (default on; kernel_ms() needs it)."""
         LB.check(LB.lib().msa_plan_set_timing(self._h, int(bool(on))), "msa_plan_set_timing")
@@ -199,6 +226,18 @@ class Plan:
             ii = np.broadcast_to(i[:, None], j.shape)
             out[ii[ok], j[ok]] = vals[ok]
         return out
+
+
+def cigar_of(ops_end_to_start: bytes) -> str:
+    """Run-length CIGAR (start -> end) of traceback ops given end -> start."""
+    out, k = [], len(ops_end_to_start) - 1
+    while k >= 0:
+        op, run = ops_end_to_start[k], 0
+        while k >= 0 and ops_end_to_start[k] == op:
+            run += 1
+            k -= 1
+        out.append(f"{run}{chr(op)}")
+    return "".join(out)
 
 
 def jlo_of(i: int, band: int) -> int:

@@ -240,6 +240,16 @@ int64_t msa_plan_stripes(const msa_plan* plan);
  * (s*pmax + t/16)*1024 + r*16 + t%16), cs_s = meta[12*(stripe0+s)].  R = 2 only
  * for two-pass single-pair SW-linear H plans. */
 int msa_plan_pair_layout(const msa_plan* plan, int64_t pair, int64_t* out4);
+/* Smith-Waterman traceback ON THE DEVICE (msa_traceback.hip), for an
+ * MSA_SW_AFFINE plan with MSA_CELLS_DIR after msa_plan_run on the same stream:
+ * one wave walks pair `pair`'s direction bytes dDir from the end cell the run
+ * found (first maximum, row-major) and writes the ops end -> start into d_ops
+ * ('M' diagonal, 'D' gap consuming B, 'I' gap consuming A; at most ops_cap,
+ * m+n suffices) and d_info[4] = {n_ops, beg_i, beg_j, status} (beg = the
+ * first aligned cell, 1-based; status 0 or MSA_ERR_CAPACITY).  Asynchronous,
+ * no host sync; tie order of the oracle's orc_sw. */
+int msa_plan_traceback(msa_plan* plan, int64_t pair, const uint8_t* dDir, uint8_t* d_ops, int64_t ops_cap,
+                       int64_t* d_info, void* stream);
 /* Order-independent digest of pair `pair`'s H cells (oracle orc_checksum_h). */
 int msa_plan_checksum(msa_plan* plan, const int32_t* dH, int64_t pair, uint64_t* digest, void* stream);
 /* Device time (ms) of the last msa_plan_run's stripe kernel, from HIP events

@@ -21,9 +21,17 @@ if wl in ("c2", "c2n"):
     cells = LB.CELLS_H if wl == "c2" else LB.CELLS_NONE
     pl = Plan(LB.SW_LINEAR, cells, [10000], [10000], [0], [0], match=1, mismatch=0, gap_open=1, gap_extend=1)
 elif wl == "c5":
-    A, B = (seqs[4] * 3)[:20000], (seqs[5] * 3)[:20000]
+    from cse305_parallel_sequence_alignment_amd import data
+
+    A, B = data.c5_pair(0, False)  # the bench's C5 pair
     pl = Plan(LB.SW_AFFINE, LB.CELLS_DIR, [20000], [20000], [0], [0], match=1, mismatch=0, gap_open=3,
               gap_extend=1, track_end=True)
+elif wl == "c3":
+    from cse305_parallel_sequence_alignment_amd import data
+
+    A, B = data.c3_pair(False)
+    pl = Plan(LB.NW_BANDED, LB.CELLS_H, [len(A)], [len(B)], [0], [0], match=1, mismatch=0, gap_open=3,
+              gap_extend=1, band=512)
 else:  # c4
     L, K = 4000, 1024
     rng = np.random.default_rng(0x5EED0004)

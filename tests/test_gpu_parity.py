@@ -424,20 +424,74 @@ def test_c3_full_size(oracle, dev, LB):
     assert pl.checksum(H) == digest
 
 
-def test_c5_fill_20k(oracle, dev, LB):
-    """C5's fill as bench.py runs it (20k x 20k affine SW, open 3 / extend 1, traceback bytes): score and end."""
+def _rescore(A, B, beg, cigar, ma, mi, go, ge):
+    """Score of the local alignment a CIGAR describes from beg (1-based): affine gaps go + (k-1) ge."""
+    import re
+
+    i, j, sc = beg[0] - 1, beg[1] - 1, 0
+    for run, op in re.findall(r"(\d+)([MID])", cigar):
+        run = int(run)
+        if op == "M":
+            sc += sum(ma if A[i + k] == B[j + k] else mi for k in range(run))
+            i, j = i + run, j + run
+        elif op == "I":
+            sc -= go + (run - 1) * ge
+            i += run
+        else:
+            sc -= go + (run - 1) * ge
+            j += run
+    return sc, (i, j)
+
+
+@pytest.mark.parametrize("which", ["c5", "dissimilar"])
+def test_c5_fill_and_device_traceback_20k(oracle, dev, LB, which):
+    """C5 as bench.py runs it: 20k x 20k affine SW (open 3 / extend 1) fill + the traceback ON THE DEVICE
+    (msa_plan_traceback): score, end, begin and the full CIGAR equal the oracle's; the CIGAR re-scores
+    to the optimum and ends at the end cell."""
     import torch
     from cse305_parallel_sequence_alignment_amd import data
     from cse305_parallel_sequence_alignment_amd.plan import Plan
 
-    A, B = data.c5_pair(0)
+    A, B = data.c5_pair(0) if which == "c5" else (data.bundled()[5][:20000], data.bundled()[0][:20000])
     pl = Plan(LB.SW_AFFINE, LB.CELLS_DIR, [len(A)], [len(B)], [0], [0], match=1, mismatch=0, gap_open=3,
               gap_extend=1, track_end=True)
     D = torch.empty(pl.cells_elems, dtype=torch.uint8, device=dev)
     pl.run(_dev(A, dev), _dev(B, dev), D)
-    o = oracle.sw(A, B, 1, 0, 3, 1)
+    tb = pl.traceback(D)
     r = pl.results()[0]
+    o = oracle.sw(A, B, 1, 0, 3, 1, want_tb=True)
     assert (r["score"], tuple(r["end"])) == (o["score"], tuple(o["end"]))
+    assert tuple(tb["beg"]) == tuple(o["beg"]) and tb["cigar"] == o["cigar"]
+    sc, stop = _rescore(A, B, tb["beg"], tb["cigar"], 1, 0, 3, 1)
+    assert sc == r["score"] and stop == tuple(r["end"])
+
+
+@pytest.mark.parametrize("m,n", [(3000, 2900), (1500, 4100), (4097, 130)])
+@pytest.mark.parametrize("scoring", [(1, 0, 3, 1), (2, -3, 5, 2), (1, -1, 1, 1)])
+def test_device_traceback_multi_stripe(oracle, dev, LB, m, n, scoring):
+    """Device traceback across many stripes and 16-step blocks (mutated copies: long paths with gaps)."""
+    import torch
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+
+    rng = np.random.default_rng(m + n)
+    A = rs(rng, m)
+    b = bytearray(A[:n] if n <= m else A + rs(rng, n - m))
+    for k in rng.choice(len(b), size=len(b) // 20, replace=False):
+        b[k] = ACGT[rng.integers(4)]
+    for k in sorted(rng.choice(len(b) - 8, size=12, replace=False), reverse=True):
+        if rng.integers(2):
+            del b[k:k + int(rng.integers(1, 6))]
+        else:
+            b[k:k] = rs(rng, int(rng.integers(1, 6)))
+    B = bytes(b)
+    ma, mi, go, ge = scoring
+    pl = Plan(LB.SW_AFFINE, LB.CELLS_DIR, [len(A)], [len(B)], [0], [0], match=ma, mismatch=mi, gap_open=go,
+              gap_extend=ge, track_end=True)
+    D = torch.empty(pl.cells_elems, dtype=torch.uint8, device=dev)
+    pl.run(_dev(A, dev), _dev(B, dev), D)
+    tb = pl.traceback(D)
+    o = oracle.sw(A, B, ma, mi, go, ge, want_tb=True)
+    assert (pl.results()[0]["score"], tuple(tb["beg"]), tb["cigar"]) == (o["score"], tuple(o["beg"]), o["cigar"])
 
 
 def test_plan_rejects_bad_buffers(dev, LB):
