@@ -180,7 +180,7 @@ def main():
             return batch.step()  # fill this rank's pairs, then RCCL all-gather of every rank's scores
     elif wl == "c5":
         tb_ops = torch.empty(m + n + 2, dtype=torch.uint8, device=dev)
-        tb_info = torch.zeros(4, dtype=torch.int64, device=dev)
+        tb_info = torch.zeros(8, dtype=torch.int64, device=dev)
 
         def step():
             plan.run(dA, dB, out)
@@ -262,6 +262,9 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         tb_ms = e0.elapsed_time(e1) / 5
+        inf = tb_info.cpu().tolist()
+        tb_walk = dict(ops=inf[0], group_switches=inf[4], fetched_on_demand=inf[5], memtime_ticks=inf[6],
+                       wait_ticks=inf[7])
     if plan.error():
         raise SystemExit(f"rank {rank}: a kernel wait hit its spin limit in the timing pass")
 
@@ -310,7 +313,8 @@ def main():
                                         f"once; no collective in the step)"),
                            score_rank0=int(res[0]["score"]), checks_all_ranks=bool(ok.item()), **checks,
                            kernel_errors=0, dp_kernel_ms=round(kern_ms, 4),
-                           **({"traceback_ms": round(tb_ms, 4)} if tb_ms is not None else {})),
+                           **({"traceback_ms": round(tb_ms, 4), "traceback_walk": tb_walk} if tb_ms is not None
+                              else {})),
             "roofline": roof,
             "cpu_baseline": cpu,
         }

@@ -10,18 +10,19 @@
 //
 // One wave walks the path from the pair's end cell (read from the reduction's
 // PairResult on the same stream, no host round trip).  Its state is uniform
-// (SGPRs); the block under the walk sits in four VGPRs per lane and a step
-// reads its byte with v_readlane from lane r -- no LDS, no per-step memory
-// access.  A diagonal step keeps t (r-1, j-1), a gap step lowers t by one, so
-// a near-diagonal path stays inside one block for up to 64 steps.  While
-// walking, the wave prefetches the block it will need next (the stripe above,
-// at the column the path will leave through, or the block to the left) into a
-// second VGPR set, so most block switches find their bytes already loaded.
+// (SGPRs); the 4 KiB group of blocks under the walk sits in LDS and a step
+// reads its byte there at a wave-uniform address.  While walking, the wave
+// prefetches the group it will need next (the stripe above, at the column the
+// path will leave through, or the group to the left, whichever boundary comes
+// first) into a second VGPR set ~24 steps ahead, so most group switches find
+// their bytes already loaded.
 // Ops are packed four per dword in an SGPR, parked in one lane of a VGPR (a
 // lane-select) and stored 256 at a time with one vector store (no scalar-cache
 // writes).
 // Output: ops from the end cell back to the start ('M' diagonal, 'D' a gap
-// consuming B, 'I' a gap consuming A), info = {n_ops, beg_i, beg_j, status}.
+// consuming B, 'I' a gap consuming A), info = {n_ops, beg_i, beg_j, status,
+// group switches, of them fetched on demand (mispredicted), s_memtime ticks of
+// the walk, of them waiting for group loads}.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -29,15 +30,49 @@
 
 namespace msa {
 
-__device__ __forceinline__ unsigned dir_byte(const uint4& v, int r, int q) {
-  // byte q (0..15) of lane r's 16-byte row segment
-  const int w = q >> 2;
-  const unsigned x = (w == 0) ? __builtin_amdgcn_readlane(v.x, r)
-                   : (w == 1) ? __builtin_amdgcn_readlane(v.y, r)
-                   : (w == 2) ? __builtin_amdgcn_readlane(v.z, r)
-                              : __builtin_amdgcn_readlane(v.w, r);
-  return (x >> ((q & 3) * 8)) & 0xffu;
+// A "group" is 4 consecutive 16-step blocks of one stripe: steps [64g, 64g + 64)
+// of all 64 rows, 4 KiB contiguous (blocks of a stripe are consecutive in
+// memory).  Lane r holds its row's 64 bytes in 16 dwords; dword k covers steps
+// 64g + 4k .. +3.  A diagonal step lowers t by 2 and r by 1, so a group serves
+// ~32 diagonal steps and a 64-row stripe takes 1-3 groups.
+// Group loads are LDS-DMA (global_load_lds_dwordx4: each lane's 16 bytes land
+// at LDS base + 16 * lane, no VGPR destination) into the second of two 4 KiB
+// staging buffers; the walk reads its byte from the current one.  They are
+// issued as inline asm so that
+// the compiler's wait-count pass does not see them -- it would otherwise drain
+// them with vmcnt(0) in front of unrelated work.  At most one group load is in
+// flight; it is waited for explicitly (s_waitcnt vmcnt(0), memory clobber, so
+// the LDS reads that follow cannot move above it) before the staging buffer is
+// read or refilled.  M0 is written in the same statement that uses it.
+__device__ __forceinline__ void glds16(const uint8_t* gsrc, unsigned lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
 }
+// Transition tables of the walk (oracle orc_sw tie order): entry (d & 15) of a 64-bit
+// constant, 4 bits {op (bits 0-1): 0 none, 1 M, 2 D, 3 I; next state (bits 2-3):
+// 0 H, 1 E, 2 F, 3 stop}.
+constexpr unsigned long long tb_lut(int st) {
+  unsigned long long v = 0;
+  for (int d = 0; d < 16; ++d) {
+    unsigned e = 0;
+    if (st == 0) {
+      const int hs = d & 3;
+      e = hs == 0 ? (3u << 2) : hs == 1 ? 1u : hs == 2 ? (1u << 2) : (2u << 2);
+    } else if (st == 1) {
+      e = 2u | ((d & 4) ? 0u : (1u << 2));
+    } else {
+      e = 3u | ((d & 8) ? 0u : (2u << 2));
+    }
+    v |= (unsigned long long)e << (4 * d);
+  }
+  return v;
+}
+constexpr unsigned long long TB_LUT_H = tb_lut(0), TB_LUT_E = tb_lut(1), TB_LUT_F = tb_lut(2);
+
+__device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" : : : "memory"); }
 
 __global__ __launch_bounds__(64) void sw_traceback_kernel(const uint8_t* __restrict__ dir,
                                                           const msa_pair_desc* __restrict__ pairs,
@@ -48,19 +83,28 @@ __global__ __launch_bounds__(64) void sw_traceback_kernel(const uint8_t* __restr
   const int lane = threadIdx.x;
   const msa_pair_desc pd = pairs[pair];
   const PairResult r0 = res[pair];
-  const uint8_t* base = dir + pd.out_off;
-  const long long pmax = pd.pmax;
-  long long i = r0.end_i, j = r0.end_j;
-  long long nops = 0;
+  const uint8_t* base = dir + pd.out_off + lane * 16;
+  const int pmax = pd.pmax;
+  int i = (int)r0.end_i, j = (int)r0.end_j;  // plans hold m, n < 2^26
+  int nops = 0;
   int st = 0;  // 0: in H, 1: in E (horizontal gap), 2: in F (vertical gap)
   int status = 0;
-  uint4 cur = make_uint4(0, 0, 0, 0), nxt = make_uint4(0, 0, 0, 0);
-  long long cur_blk = -1, nxt_blk = -1;
-  long long s_cached = -1;
+  __shared__ __attribute__((aligned(16))) uint8_t stage[2][4096];  // current group / the one being fetched
+  typedef __attribute__((address_space(3))) uint8_t lds_u8;
+  const unsigned stage_lds = (unsigned)(uintptr_t)(lds_u8*)&stage[0][0];
+  int cb = 0;  // stage[cb] holds the current group, stage[cb ^ 1] receives the next
+  long long cur_key = -1, nxt_key = -1;  // s * 2^32 + g
+  bool pend = false;                     // a group load into `stage` is in flight
+  int s_cached = -1;
   int cs = 0, cs_up = 0;
-  unsigned word = 0;                     // four ops, byte k = op 4q + k
-  unsigned parked = 0;                   // this lane's dword of the 256-op buffer
+  // Ops are packed four per dword (byte k = op 4q + k) in `word`; every fourth op
+  // parks the dword in lane (q mod 64) of `parked` (a lane select: a per-lane branch
+  // would push the walk's uniform state into VGPRs), and every 256th op stores the
+  // 64 parked dwords with one vector store.
+  unsigned word = 0;
+  unsigned parked = 0;
   // store the parked dwords of the 256-op group starting at g0, up to op `upto`
+  // (the final, partial group; outside the walk, so its per-lane branch is harmless)
   auto flush = [&](long long g0, long long upto) {
     const long long o = g0 + 4ll * lane;
     if (o >= upto) return;
@@ -70,84 +114,128 @@ __global__ __launch_bounds__(64) void sw_traceback_kernel(const uint8_t* __restr
       for (int k = 0; k < 4 && o + k < cap; ++k) ops[o + k] = (uint8_t)(parked >> (8 * k));
     }
   };
-  auto emit = [&](unsigned op) {
-    word |= op << (8 * (nops & 3));
-    ++nops;
-    if ((nops & 3) == 0) {
-      if (lane == (int)(((nops - 4) >> 2) & 63)) parked = word;
-      word = 0;
-      if ((nops & 255) == 0) flush(nops - 256, nops);
-    }
+  auto key_of = [](int s, int g) { return ((long long)s << 32) | (unsigned)g; };
+  // issue the 4 block loads of group (s, g) into stage[cb ^ 1] (blocks past the stripe's
+  // pmax are not loaded, so no read leaves the pair's direction bytes)
+  auto issue_group = [&](int s, int g) {
+    const long long blk0 = (long long)s * pmax + 4ll * g;
+    const unsigned dst = stage_lds + 4096u * (unsigned)(cb ^ 1);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (4 * g + q < pmax) glds16(base + (blk0 + q) * 1024, dst + 1024u * q);
+  };
+  int n_switch = 0, n_sync = 0;               // group switches, of them fetched on demand
+  long long t_wait = 0;                        // clock ticks spent waiting for group loads
+  const long long t_begin = (long long)__builtin_amdgcn_s_memtime();
+  auto timed_wait = [&]() {
+    const long long a = (long long)__builtin_amdgcn_s_memtime();
+    vm_wait_all();
+    t_wait += (long long)__builtin_amdgcn_s_memtime() - a;
   };
   if (r0.score > 0) {
-    while (i > 0 && j > 0) {
-      const long long s = (i - 1) >> 6;
-      const int r = (int)((i - 1) & 63);
+    bool stopped = false;
+    // outer iteration: make the group under (i, j) current, keep the next one in flight,
+    // then run the steps that provably stay inside the group without any further checks
+    while (i > 0 && j > 0 && !stopped && nops <= cap) {
+      const int s = (i - 1) >> 6;
+      int r = (i - 1) & 63;
       if (s != s_cached) {
         cs = meta[pd.stripe0 + s].cs;
         cs_up = s > 0 ? meta[pd.stripe0 + s - 1].cs : 0;
         s_cached = s;
       }
-      const long long t = j - cs + r;
-      const long long blk = s * pmax + (t >> 4);
-      if (blk != cur_blk) {
-        if (blk == nxt_blk) {
-          cur = nxt;
-          cur_blk = nxt_blk;
-          nxt_blk = -1;
+      int t = j - cs + r;
+      const int g = t >> 6;
+      const long long key = key_of(s, g);
+      if (key != cur_key) {
+        ++n_switch;
+        if (pend) {
+          timed_wait();
+          pend = false;
+          if (key != nxt_key) issue_group(s, g), timed_wait(), ++n_sync;  // mispredicted: fetch now
         } else {
-          cur = *(const uint4*)(base + blk * 1024 + lane * 16);
-          cur_blk = blk;
+          issue_group(s, g);
+          timed_wait();
+          ++n_sync;
         }
+        nxt_key = -1;
+        cb ^= 1;  // the fetched group becomes current
+        cur_key = key;
       }
-      // prefetch the block the walk will need next: near the top rows, the stripe above
-      // at the column a diagonal path leaves through; near the block's left edge, the
-      // block to the left
+      // steps that stay in this group: each lowers r by <= 1 and t by <= 2
+      const int to_top = r + 1, to_left = ((t & 63) >> 1) + 1;
+      const int budget = to_top < to_left ? to_top : to_left;
+      // prefetch the group the walk leaves into: the stripe above (at the column a
+      // diagonal path exits through) if the top row comes first, else the group to the left
       long long want = -1;
-      if (r < 12 && s > 0) {
-        const long long tu = (j - r) - cs_up + 63;
-        if (tu >= 0) want = (s - 1) * pmax + (tu >> 4);
-      } else if ((t & 15) < 3 && (t >> 4) > 0) {
-        want = blk - 1;
-      }
-      if (want >= 0 && want != nxt_blk && want != cur_blk) {
-        nxt = *(const uint4*)(base + want * 1024 + lane * 16);
-        nxt_blk = want;
-      }
-      const unsigned d = dir_byte(cur, r, (int)(t & 15));
-      if (st == 0) {
-        const unsigned hs = d & 3u;
-        if (hs == 0) break;  // local start
-        if (hs == 1) {
-          emit('M');
-          --i;
-          --j;
-        } else {
-          st = (hs == 2) ? 1 : 2;
+      int ws = 0, wg = 0;
+      if (to_top <= to_left) {
+        const int tu = (j - r) - cs_up + 63;
+        if (s > 0 && tu >= 0) {
+          ws = s - 1;
+          wg = tu >> 6;
+          want = key_of(ws, wg);
         }
-      } else if (st == 1) {
-        emit('D');
-        st = (d & 4u) ? 0 : 1;
-        --j;
-      } else {
-        emit('I');
-        st = (d & 8u) ? 0 : 2;
-        --i;
+      } else if (g > 0) {
+        ws = s;
+        wg = g - 1;
+        want = key_of(ws, wg);
       }
-      if (nops > cap) {
-        status = -8;  // MSA_ERR_CAPACITY
-        break;
+      if (want >= 0 && want != nxt_key && want != cur_key) {
+        if (pend) timed_wait();  // stage[cb ^ 1] is about to be refilled
+        issue_group(ws, wg);
+        nxt_key = want;
+        pend = true;
+      }
+      const uint8_t* grp = &stage[cb][0];
+      // branch-free step: a 4-bit transition entry {op: 0 none / 1 M / 2 D / 3 I, next state:
+      // 0 H, 1 E, 2 F, 3 stop} looked up by (state, low 4 bits of the byte) in three 64-bit
+      // constants (16 entries each); only the loop test and the 4th-op parking branch
+      unsigned long long lut = st == 0 ? TB_LUT_H : st == 1 ? TB_LUT_E : TB_LUT_F;
+      int k = 0;
+      for (; k < budget; ++k) {
+        // the byte of cell (r, t): block (t >> 4) & 3 of the group, row r, step t & 15 --
+        // one LDS read at a wave-uniform address (a broadcast), made scalar
+        const unsigned d = __builtin_amdgcn_readfirstlane((unsigned)grp[(((t >> 4) & 3) << 10) + (r << 4) + (t & 15)]);
+        const unsigned e = (unsigned)(lut >> (4 * (d & 15u))) & 15u;
+        const unsigned op = e & 3u, nst = e >> 2;
+        const int di = (int)(op & 1u), dj = (int)((op ^ (op >> 1)) & 1u);
+        i -= di;
+        j -= dj;
+        r -= di;
+        t -= di + dj;
+        word |= ((0x49444D00u >> (8 * op)) & 0xffu) << (8 * (nops & 3));
+        nops += op != 0u;
+        if (op != 0u && (nops & 3) == 0) {
+          const int slot = ((nops - 4) >> 2) & 63;
+          parked = (lane == slot) ? word : parked;
+          word = 0;
+          if ((nops & 255) == 0 && nops <= cap) *(unsigned*)(ops + (nops - 256) + 4 * lane) = parked;
+        }
+        st = (int)nst;
+        lut = nst == 0u ? TB_LUT_H : nst == 1u ? TB_LUT_E : TB_LUT_F;
+        if (nst == 3u || i <= 0 || j <= 0) break;
+      }
+      if (st == 3) {  // local start (H came from 0): the walk ends at this cell
+        st = 0;
+        stopped = true;
       }
     }
+    if (nops > cap) status = -8;  // MSA_ERR_CAPACITY
   }
+  if (pend) vm_wait_all();  // no load left in flight when the wave ends
   // flush the partial word and the parked dwords of the last (partial) 256-op group
-  if ((nops & 3) && lane == (int)((nops >> 2) & 63)) parked = word;
+  if (nops & 3) parked = (lane == ((nops >> 2) & 63)) ? word : parked;
   if (nops & 255) flush(nops & ~255ll, nops);
   if (lane == 0) {
     info[0] = nops;
     info[1] = i + 1;
     info[2] = j + 1;
     info[3] = status;
+    info[4] = n_switch;
+    info[5] = n_sync;
+    info[6] = (long long)__builtin_amdgcn_s_memtime() - t_begin;  // s_memtime ticks, whole walk
+    info[7] = t_wait;
   }
 }
 

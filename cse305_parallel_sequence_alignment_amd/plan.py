@@ -160,8 +160,8 @@ class Plan:
             raise ValueError("dDir must be the uint8 CUDA tensor the plan's run() wrote")
         if not (d_ops.is_cuda and d_ops.dtype == torch.uint8 and d_ops.is_contiguous()):
             raise ValueError("d_ops must be a contiguous uint8 CUDA tensor")
-        if not (d_info.is_cuda and d_info.dtype == torch.int64 and d_info.numel() >= 4):
-            raise ValueError("d_info must be an int64 CUDA tensor of >= 4 elements")
+        if not (d_info.is_cuda and d_info.dtype == torch.int64 and d_info.numel() >= 8):
+            raise ValueError("d_info must be an int64 CUDA tensor of >= 8 elements")
         LB.check(LB.lib().msa_plan_traceback(self._h, pair, _ptr(dDir), _ptr(d_ops), d_ops.numel(), _ptr(d_info),
                                              _stream_ptr(stream)), "msa_plan_traceback")
 
@@ -171,12 +171,13 @@ class Plan:
 
         dev = dDir.device
         ops = torch.empty(self.ms[pair] + self.ns[pair] + 2, dtype=torch.uint8, device=dev)
-        info = torch.zeros(4, dtype=torch.int64, device=dev)
+        info = torch.zeros(8, dtype=torch.int64, device=dev)
         self.traceback_async(dDir, ops, info, pair, stream)
         inf = info.cpu().tolist()
         LB.check(int(inf[3]), "msa_plan_traceback")
         o = bytes(ops[:inf[0]].cpu().numpy().tobytes())
-        return dict(ops=o, beg=(int(inf[1]), int(inf[2])), cigar=cigar_of(o))
+        return dict(ops=o, beg=(int(inf[1]), int(inf[2])), cigar=cigar_of(o),
+                    stats=dict(switches=int(inf[4]), on_demand=int(inf[5]), ticks=int(inf[6]), wait_ticks=int(inf[7])))
 
     def set_timing(self, on: bool) -> None:
         """Record HIP events around the DP kernel in run() (default on; kernel_ms() needs it)."""

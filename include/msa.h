@@ -245,8 +245,10 @@ int msa_plan_pair_layout(const msa_plan* plan, int64_t pair, int64_t* out4);
  * one wave walks pair `pair`'s direction bytes dDir from the end cell the run
  * found (first maximum, row-major) and writes the ops end -> start into d_ops
  * ('M' diagonal, 'D' gap consuming B, 'I' gap consuming A; at most ops_cap,
- * m+n suffices) and d_info[4] = {n_ops, beg_i, beg_j, status} (beg = the
- * first aligned cell, 1-based; status 0 or MSA_ERR_CAPACITY).  Asynchronous,
+ * m+n suffices) and d_info[8] = {n_ops, beg_i, beg_j, status, group
+ * switches, of them fetched on demand, s_memtime ticks of the walk, of them
+ * waiting for loads} (beg = the first aligned cell, 1-based; status 0 or
+ * MSA_ERR_CAPACITY).  Asynchronous,
  * no host sync; tie order of the oracle's orc_sw. */
 int msa_plan_traceback(msa_plan* plan, int64_t pair, const uint8_t* dDir, uint8_t* d_ops, int64_t ops_cap,
                        int64_t* d_info, void* stream);
