@@ -162,9 +162,12 @@ __global__ __launch_bounds__(64) void sw_traceback_kernel(const uint8_t* __restr
         cb ^= 1;  // the fetched group becomes current
         cur_key = key;
       }
-      // steps that stay in this group: each lowers r by <= 1 and t by <= 2
+      // steps that stay in this group (each lowers r by <= 1 and t by <= 2) and inside the
+      // matrix (i and j drop by <= 1 per step)
       const int to_top = r + 1, to_left = ((t & 63) >> 1) + 1;
-      const int budget = to_top < to_left ? to_top : to_left;
+      int budget = to_top < to_left ? to_top : to_left;
+      budget = budget < i ? budget : i;
+      budget = budget < j ? budget : j;
       // prefetch the group the walk leaves into: the stripe above (at the column a
       // diagonal path exits through) if the top row comes first, else the group to the left
       long long want = -1;
@@ -192,16 +195,14 @@ __global__ __launch_bounds__(64) void sw_traceback_kernel(const uint8_t* __restr
       // 0 H, 1 E, 2 F, 3 stop} looked up by (state, low 4 bits of the byte) in three 64-bit
       // constants (16 entries each); only the loop test and the 4th-op parking branch
       unsigned long long lut = st == 0 ? TB_LUT_H : st == 1 ? TB_LUT_E : TB_LUT_F;
-      int k = 0;
-      for (; k < budget; ++k) {
+      const int r_in = r, t_in = t;
+      for (int k = 0; k < budget; ++k) {
         // the byte of cell (r, t): block (t >> 4) & 3 of the group, row r, step t & 15 --
         // one LDS read at a wave-uniform address (a broadcast), made scalar
-        const unsigned d = __builtin_amdgcn_readfirstlane((unsigned)grp[(((t >> 4) & 3) << 10) + (r << 4) + (t & 15)]);
+        const unsigned d = __builtin_amdgcn_readfirstlane((unsigned)grp[(((t >> 4) & 3) << 10) | (r << 4) | (t & 15)]);
         const unsigned e = (unsigned)(lut >> (4 * (d & 15u))) & 15u;
         const unsigned op = e & 3u, nst = e >> 2;
         const int di = (int)(op & 1u), dj = (int)((op ^ (op >> 1)) & 1u);
-        i -= di;
-        j -= dj;
         r -= di;
         t -= di + dj;
         word |= ((0x49444D00u >> (8 * op)) & 0xffu) << (8 * (nops & 3));
@@ -214,8 +215,10 @@ __global__ __launch_bounds__(64) void sw_traceback_kernel(const uint8_t* __restr
         }
         st = (int)nst;
         lut = nst == 0u ? TB_LUT_H : nst == 1u ? TB_LUT_E : TB_LUT_F;
-        if (nst == 3u || i <= 0 || j <= 0) break;
+        if (nst == 3u) break;
       }
+      i -= r_in - r;                  // rows consumed
+      j -= (t_in - t) - (r_in - r);   // columns consumed
       if (st == 3) {  // local start (H came from 0): the walk ends at this cell
         st = 0;
         stopped = true;
