@@ -259,3 +259,33 @@ def test_main_alignment_non_integral(oracle, dev, dataset):
         want, wsc = oracle.main_alignment_text(A, B, g, h)
         got, sc = api.main_alignment_text(b"\0" + A, b"\0" + B, len(A), len(B), 8, g, h)
         assert got == want and sc == wsc
+
+
+def test_harness_drivers(oracle, dev, dataset, tmp_path):
+    """The build-owned harness (harness.py, testing.cpp's drivers): with rand() replayed from srand(1)
+    the single-threaded driver draws known pairs and prints the oracle's text for each; the threaded
+    drivers write the reference's CSV layouts."""
+    import io
+
+    from cse305_parallel_sequence_alignment_amd import harness as H
+
+    names, seqs = [], []
+    assert H.read_and_store_sequences(names, seqs) == 0
+    H.c_srand(1)
+    picks = [(H.c_rand() % 19, H.c_rand() % 19) for _ in range(5)]
+    H.c_srand(1)
+    out = io.StringIO()
+    assert H.test_input_size_thread(names, seqs, test_pairs=5, input_size=300, threads=1,
+                                    csv_path=str(tmp_path / "in.csv"), out=out) == 0
+    want = "".join(oracle.main_alignment_text(seqs[a][:300], seqs[b][:300])[0] for a, b in picks)
+    assert out.getvalue() == want
+    rows = (tmp_path / "in.csv").read_text().splitlines()
+    assert rows[:2] == ["Testing with different input sizes", "Test number,Input size,Execution time"]
+    assert [r.split(",")[:2] for r in rows[2:]] == [[str(k), "300"] for k in range(5)]
+    assert H.test_similarity(names, seqs, test_pairs=8, threads=4, csv_path=str(tmp_path / "sim.csv"),
+                             max_len=400, out=io.StringIO()) == 0
+    rows = (tmp_path / "sim.csv").read_text().splitlines()
+    assert rows[1] == "Test number,Similarity,Execution time" and len(rows) == 10
+    assert H.test_n_cores_thread(names, seqs, test_pairs=6, threads=3, csv_path=str(tmp_path / "nc.csv"),
+                                 max_len=200, out=io.StringIO()) == 0
+    assert len((tmp_path / "nc.csv").read_text().splitlines()) == 8
