@@ -14,8 +14,9 @@
 // reads its byte there at a wave-uniform address.  While walking, the wave
 // prefetches the group it will need next (the stripe above, at the column the
 // path will leave through, or the group to the left, whichever boundary comes
-// first) into a second VGPR set ~24 steps ahead, so most group switches find
-// their bytes already loaded.
+// first) into a second staging buffer, so most group switches find their bytes
+// already loaded.  Inside a group, one LDS read fetches an 8x8 window of bytes
+// (one per lane) and up to 7 steps are resolved from it with v_readlane.
 // Ops are packed four per dword in an SGPR, parked in one lane of a VGPR (a
 // lane-select) and stored 256 at a time with one vector store (no scalar-cache
 // writes).
@@ -193,29 +194,45 @@ __global__ __launch_bounds__(64) void sw_traceback_kernel(const uint8_t* __restr
       const uint8_t* grp = &stage[cb][0];
       // branch-free step: a 4-bit transition entry {op: 0 none / 1 M / 2 D / 3 I, next state:
       // 0 H, 1 E, 2 F, 3 stop} looked up by (state, low 4 bits of the byte) in three 64-bit
-      // constants (16 entries each); only the loop test and the 4th-op parking branch
+      // constants (16 entries each); only the loop tests and the 4th-op parking branch
       unsigned long long lut = st == 0 ? TB_LUT_H : st == 1 ? TB_LUT_E : TB_LUT_F;
       const int r_in = r, t_in = t;
-      for (int k = 0; k < budget; ++k) {
-        // the byte of cell (r, t): block (t >> 4) & 3 of the group, row r, step t & 15 --
-        // one LDS read at a wave-uniform address (a broadcast), made scalar
-        const unsigned d = __builtin_amdgcn_readfirstlane((unsigned)grp[(((t >> 4) & 3) << 10) | (r << 4) | (t & 15)]);
-        const unsigned e = (unsigned)(lut >> (4 * (d & 15u))) & 15u;
-        const unsigned op = e & 3u, nst = e >> 2;
-        const int di = (int)(op & 1u), dj = (int)((op ^ (op >> 1)) & 1u);
-        r -= di;
-        t -= di + dj;
-        word |= ((0x49444D00u >> (8 * op)) & 0xffu) << (8 * (nops & 3));
-        nops += op != 0u;
-        if (op != 0u && (nops & 3) == 0) {
-          const int slot = ((nops - 4) >> 2) & 63;
-          parked = (lane == slot) ? word : parked;
-          word = 0;
-          if ((nops & 255) == 0 && nops <= cap) *(unsigned*)(ops + (nops - 256) + 4 * lane) = parked;
+      // The budget's steps run in windows of up to 7: one LDS read gives lane (a, b) =
+      // (lane >> 3, lane & 7) the byte of cell (i - a, j - b), i.e. (r - a, t - a - b) in the
+      // group, and the steps then pick their bytes with v_readlane at a scalar lane index
+      // (no LDS latency per step).  Seven steps move at most 7 in i and in j, so every cell
+      // they visit is in the window; the budget keeps them inside the group.
+      const int wa = lane >> 3, wb = lane & 7;
+      bool stop = false;
+      while (budget > 0 && !stop) {
+        const int kmax = budget < 7 ? budget : 7;
+        const int rr = r - wa, tt = t - wa - wb;
+        const bool in_grp = rr >= 0 && (tt >> 6) == (t >> 6);
+        const int win = in_grp ? (int)grp[(((tt >> 4) & 3) << 10) | (rr << 4) | (tt & 15)] : 0;
+        int ca = 0, cbw = 0;  // window offsets (a, b) of the walk's cell
+        int k = 0;
+        for (; k < kmax; ++k) {
+          const unsigned d = (unsigned)__builtin_amdgcn_readlane(win, (ca << 3) | cbw);
+          const unsigned e = (unsigned)(lut >> (4 * (d & 15u))) & 15u;
+          const unsigned op = e & 3u, nst = e >> 2;
+          const int di = (int)(op & 1u), dj = (int)((op ^ (op >> 1)) & 1u);
+          ca += di;
+          cbw += dj;
+          word |= ((0x49444D00u >> (8 * op)) & 0xffu) << (8 * (nops & 3));
+          nops += op != 0u;
+          if (op != 0u && (nops & 3) == 0) {
+            const int slot = ((nops - 4) >> 2) & 63;
+            parked = (lane == slot) ? word : parked;
+            word = 0;
+            if ((nops & 255) == 0 && nops <= cap) *(unsigned*)(ops + (nops - 256) + 4 * lane) = parked;
+          }
+          st = (int)nst;
+          lut = nst == 0u ? TB_LUT_H : nst == 1u ? TB_LUT_E : TB_LUT_F;
+          if (nst == 3u) { ++k; stop = true; break; }
         }
-        st = (int)nst;
-        lut = nst == 0u ? TB_LUT_H : nst == 1u ? TB_LUT_E : TB_LUT_F;
-        if (nst == 3u) break;
+        r -= ca;
+        t -= ca + cbw;
+        budget -= k;
       }
       i -= r_in - r;                  // rows consumed
       j -= (t_in - t) - (r_in - r);   // columns consumed
