@@ -17,9 +17,8 @@
 // first) into a second staging buffer, so most group switches find their bytes
 // already loaded.  Inside a group, one LDS read fetches an 8x8 window of bytes
 // (one per lane) and up to 7 steps are resolved from it with v_readlane.
-// Ops are packed four per dword in an SGPR, parked in one lane of a VGPR (a
-// lane-select) and stored 256 at a time with one vector store (no scalar-cache
-// writes).
+// Steps are recorded as nibbles, one word per window, in an LDS ring that is
+// decoded into op bytes by the whole wave in parallel (no scalar-cache writes).
 // Output: ops from the end cell back to the start ('M' diagonal, 'D' a gap
 // consuming B, 'I' a gap consuming A), info = {n_ops, beg_i, beg_j, status,
 // group switches, of them fetched on demand (mispredicted), s_memtime ticks of
@@ -52,26 +51,14 @@ __device__ __forceinline__ void glds16(const uint8_t* gsrc, unsigned lds_dst) {
                : "v"(gsrc), "s"(lds_dst)
                : "memory");
 }
-// Transition tables of the walk (oracle orc_sw tie order): entry (d & 15) of a 64-bit
-// constant, 4 bits {op (bits 0-1): 0 none, 1 M, 2 D, 3 I; next state (bits 2-3):
-// 0 H, 1 E, 2 F, 3 stop}.
-constexpr unsigned long long tb_lut(int st) {
-  unsigned long long v = 0;
-  for (int d = 0; d < 16; ++d) {
-    unsigned e = 0;
-    if (st == 0) {
-      const int hs = d & 3;
-      e = hs == 0 ? (3u << 2) : hs == 1 ? 1u : hs == 2 ? (1u << 2) : (2u << 2);
-    } else if (st == 1) {
-      e = 2u | ((d & 4) ? 0u : (1u << 2));
-    } else {
-      e = 3u | ((d & 8) ? 0u : (2u << 2));
-    }
-    v |= (unsigned long long)e << (4 * d);
-  }
-  return v;
-}
-constexpr unsigned long long TB_LUT_H = tb_lut(0), TB_LUT_E = tb_lut(1), TB_LUT_F = tb_lut(2);
+// Transitions of the walk (oracle orc_sw tie order), by state:
+//  H: the low two bits hs of the byte -- 0 local start (stop), 1 diagonal ('M', stay in H),
+//     2 from E (no op, go to E), 3 from F (no op, go to F);
+//  E: 'D' (a gap consuming B), back to H if bit 2 (E opened from H(i, j-1)), else stay;
+//  F: 'I' (a gap consuming A), back to H if bit 3 (F opened from H(i-1, j)), else stay.
+// A transition field is (lane step: 9 M / 1 D / 8 I / 0 none) | (9 x next state, 27 = stop)
+// << 4; TB_FH holds the four H fields at 16-bit spacing, indexed by hs.
+constexpr unsigned long long TB_FH = (27ull << 4) | (9ull << 16) | ((9ull << 4) << 32) | ((18ull << 4) << 48);
 
 __device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" : : : "memory"); }
 
@@ -98,22 +85,46 @@ __global__ __launch_bounds__(64) void sw_traceback_kernel(const uint8_t* __restr
   bool pend = false;                     // a group load into `stage` is in flight
   int s_cached = -1;
   int cs = 0, cs_up = 0;
-  // Ops are packed four per dword (byte k = op 4q + k) in `word`; every fourth op
-  // parks the dword in lane (q mod 64) of `parked` (a lane select: a per-lane branch
-  // would push the walk's uniform state into VGPRs), and every 256th op stores the
-  // 64 parked dwords with one vector store.
-  unsigned word = 0;
-  unsigned parked = 0;
-  // store the parked dwords of the 256-op group starting at g0, up to op `upto`
-  // (the final, partial group; outside the walk, so its per-lane branch is harmless)
-  auto flush = [&](long long g0, long long upto) {
-    const long long o = g0 + 4ll * lane;
-    if (o >= upto) return;
-    if (o + 4 <= cap) {
-      *(unsigned*)(ops + o) = parked;
-    } else {
-      for (int k = 0; k < 4 && o + k < cap; ++k) ops[o + k] = (uint8_t)(parked >> (8 * k));
+  // every stripe's start column, staged in LDS once (a stripe change then costs an LDS
+  // read, not a ~1 us dependent global load); pairs with more stripes read the rest from HBM
+  constexpr int TB_CSL = 8192;
+  __shared__ int csl[TB_CSL];
+  const int S = (pd.m + 63) / 64;
+  for (int k = lane; k < S && k < TB_CSL; k += 64) csl[k] = meta[pd.stripe0 + k].cs;
+  auto cs_of = [&](int k) {  // wave-uniform (readfirstlane: an LDS value is otherwise "divergent")
+    return k < TB_CSL ? __builtin_amdgcn_readfirstlane(csl[k]) : meta[pd.stripe0 + k].cs;
+  };
+  // The walk records, per window of <= 7 steps, one word: nibble k = the lane step of
+  // step k (9 'M', 1 'D', 8 'I', 0 no op), steps in bits 28-31.  The words go to an LDS
+  // ring (all lanes store the same word: no per-lane branch in the walk); when it is
+  // full, and at the end, decode() turns them into op bytes in parallel (one word per
+  // lane, a wave prefix sum of the op counts) and appends them to `ops`.
+  constexpr int TB_RAW = 4096;
+  __shared__ unsigned rawl[TB_RAW];
+  int nw = 0;
+  auto decode = [&]() {
+    for (int b0 = 0; b0 < nw; b0 += 64) {
+      const unsigned w = (b0 + lane < nw) ? rawl[b0 + lane] : 0u;
+      const int k = (int)(w >> 28);
+      int c = 0;
+      for (int q = 0; q < k; ++q) c += ((w >> (4 * q)) & 15u) != 0u;
+      int incl = c;  // inclusive prefix sum over the lanes
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(incl, off);
+        if (lane >= off) incl += y;
+      }
+      long long o = nops + incl - c;
+      for (int q = 0; q < k; ++q) {
+        const unsigned dl = (w >> (4 * q)) & 15u;
+        if (dl != 0u) {
+          if (o < cap) ops[o] = dl == 9u ? 'M' : (dl == 1u ? 'D' : 'I');
+          ++o;
+        }
+      }
+      nops += __shfl(incl, 63);
     }
+    nw = 0;
   };
   auto key_of = [](int s, int g) { return ((long long)s << 32) | (unsigned)g; };
   // issue the 4 block loads of group (s, g) into stage[cb ^ 1] (blocks past the stripe's
@@ -137,12 +148,12 @@ __global__ __launch_bounds__(64) void sw_traceback_kernel(const uint8_t* __restr
     bool stopped = false;
     // outer iteration: make the group under (i, j) current, keep the next one in flight,
     // then run the steps that provably stay inside the group without any further checks
-    while (i > 0 && j > 0 && !stopped && nops <= cap) {
+    while (i > 0 && j > 0 && !stopped) {
       const int s = (i - 1) >> 6;
       int r = (i - 1) & 63;
       if (s != s_cached) {
-        cs = meta[pd.stripe0 + s].cs;
-        cs_up = s > 0 ? meta[pd.stripe0 + s - 1].cs : 0;
+        cs = cs_of(s);
+        cs_up = s > 0 ? cs_of(s - 1) : 0;
         s_cached = s;
       }
       int t = j - cs + r;
@@ -192,48 +203,44 @@ __global__ __launch_bounds__(64) void sw_traceback_kernel(const uint8_t* __restr
         pend = true;
       }
       const uint8_t* grp = &stage[cb][0];
-      // branch-free step: a 4-bit transition entry {op: 0 none / 1 M / 2 D / 3 I, next state:
-      // 0 H, 1 E, 2 F, 3 stop} looked up by (state, low 4 bits of the byte) in three 64-bit
-      // constants (16 entries each); only the loop tests and the 4th-op parking branch
-      unsigned long long lut = st == 0 ? TB_LUT_H : st == 1 ? TB_LUT_E : TB_LUT_F;
       const int r_in = r, t_in = t;
-      // The budget's steps run in windows of up to 7: one LDS read gives lane (a, b) =
-      // (lane >> 3, lane & 7) the byte of cell (i - a, j - b), i.e. (r - a, t - a - b) in the
-      // group, and the steps then pick their bytes with v_readlane at a scalar lane index
-      // (no LDS latency per step).  Seven steps move at most 7 in i and in j, so every cell
-      // they visit is in the window; the budget keeps them inside the group.
+      // The budget's steps run in windows of up to 7.  One LDS read gives lane (a, b) =
+      // (lane >> 3, lane & 7) the direction byte of cell (i - a, j - b) -- (r - a, t - a - b) in
+      // the group -- and the lane turns it into a transition word: for each state s (bits 9s..)
+      // the lane step of the move (4 bits: 9 M, 1 D, 8 I, 0 none) and 9 x the next state (5
+      // bits; 27 = local start, stop), in the oracle's tie order (tb_lut).  A step is then a
+      // v_readlane of the word at the walk's lane index plus four scalar ops; seven steps stay
+      // inside the 8 x 8 window, the budget keeps them inside the group.
       const int wa = lane >> 3, wb = lane & 7;
       bool stop = false;
+      int sh = 9 * st;
       while (budget > 0 && !stop) {
         const int kmax = budget < 7 ? budget : 7;
         const int rr = r - wa, tt = t - wa - wb;
         const bool in_grp = rr >= 0 && (tt >> 6) == (t >> 6);
-        const int win = in_grp ? (int)grp[(((tt >> 4) & 3) << 10) | (rr << 4) | (tt & 15)] : 0;
-        int ca = 0, cbw = 0;  // window offsets (a, b) of the walk's cell
-        int k = 0;
+        const unsigned dv = in_grp ? (unsigned)grp[(((tt >> 4) & 3) << 10) | (rr << 4) | (tt & 15)] : 0u;
+        const unsigned fH = (unsigned)(TB_FH >> (16 * (dv & 3u))) & 0x1ffu;
+        const unsigned fE = 1u | ((dv & 4u) ? 0u : (9u << 4));
+        const unsigned fF = 8u | ((dv & 8u) ? 0u : (18u << 4));
+        const int wt = (int)(fH | (fE << 9) | (fF << 18));
+        int idx = 0, k = 0;
+        unsigned wcode = 0;
         for (; k < kmax; ++k) {
-          const unsigned d = (unsigned)__builtin_amdgcn_readlane(win, (ca << 3) | cbw);
-          const unsigned e = (unsigned)(lut >> (4 * (d & 15u))) & 15u;
-          const unsigned op = e & 3u, nst = e >> 2;
-          const int di = (int)(op & 1u), dj = (int)((op ^ (op >> 1)) & 1u);
-          ca += di;
-          cbw += dj;
-          word |= ((0x49444D00u >> (8 * op)) & 0xffu) << (8 * (nops & 3));
-          nops += op != 0u;
-          if (op != 0u && (nops & 3) == 0) {
-            const int slot = ((nops - 4) >> 2) & 63;
-            parked = (lane == slot) ? word : parked;
-            word = 0;
-            if ((nops & 255) == 0 && nops <= cap) *(unsigned*)(ops + (nops - 256) + 4 * lane) = parked;
-          }
-          st = (int)nst;
-          lut = nst == 0u ? TB_LUT_H : nst == 1u ? TB_LUT_E : TB_LUT_F;
-          if (nst == 3u) { ++k; stop = true; break; }
+          const unsigned f = (unsigned)__builtin_amdgcn_readlane(wt, idx) >> sh;
+          const unsigned dl = f & 15u;
+          sh = (int)((f >> 4) & 31u);
+          idx += (int)dl;
+          wcode |= dl << (4 * k);
+          if (sh == 27) { ++k; stop = true; break; }
         }
-        r -= ca;
-        t -= ca + cbw;
+        rawl[nw] = wcode | ((unsigned)k << 28);  // every lane stores the same word
+        if (++nw == TB_RAW) decode();
+        const int da = idx >> 3, db = idx & 7;
+        r -= da;
+        t -= da + db;
         budget -= k;
       }
+      st = stop ? 3 : sh / 9;
       i -= r_in - r;                  // rows consumed
       j -= (t_in - t) - (r_in - r);   // columns consumed
       if (st == 3) {  // local start (H came from 0): the walk ends at this cell
@@ -241,12 +248,10 @@ __global__ __launch_bounds__(64) void sw_traceback_kernel(const uint8_t* __restr
         stopped = true;
       }
     }
-    if (nops > cap) status = -8;  // MSA_ERR_CAPACITY
   }
+  decode();  // the words still in the ring
+  if (nops > cap) status = -8;  // MSA_ERR_CAPACITY
   if (pend) vm_wait_all();  // no load left in flight when the wave ends
-  // flush the partial word and the parked dwords of the last (partial) 256-op group
-  if (nops & 3) parked = (lane == ((nops >> 2) & 63)) ? word : parked;
-  if (nops & 255) flush(nops & ~255ll, nops);
   if (lane == 0) {
     info[0] = nops;
     info[1] = i + 1;
