@@ -372,6 +372,38 @@ __device__ __forceinline__ unsigned step(const msa_kparams& kp, LaneState<ALG>& 
   return dir;
 }
 
+// Banded Gotoh (MSA_ALG_NWA) edges without per-step range masks.  A lane runs the
+// bare recurrence on every step, also outside its row's band [tmin, tmax]; those
+// values reach an in-band cell only through two cells, fixed up here:
+//  * t == tmin - 1 (column jlo - 1: out of band, or the border column 0 when jlo = 1):
+//    the state becomes the left border LB, so the row's first cell sees the exact
+//    left neighbour (and the row below, whose first cell takes its diagonal from
+//    column jlo - 1 only when that is the border column, the exact border value);
+//  * t == tmax + 1 (column jhi + 1): H and T3 become -inf, the "up" of the row
+//    below's last in-band cell (and of the next stripe's lane 0).
+// Everything else a lane computes outside its band feeds only out-of-band cells (the
+// row below starts and ends one column later), so in-band H, the hand-offs read at
+// in-band cells and the final cell equal the masked recurrence's.  FIN captures the
+// final cell at t == tmax.  Cost: 2 compares + 5 selects per step, against ~13 for
+// the range masks -- and for a band the masked head phases are the chain's
+// critical path (stripe k+1 starts ~9 phases into stripe k).
+template <bool FIN>
+__device__ __forceinline__ void band_fix(LaneState<MSA_ALG_NWA>& L, int t, int (&carry)[3]) {
+  const bool fl = (t == L.tmin - 1);
+#pragma unroll
+  for (int v = 0; v < 3; ++v) L.S[v] = fl ? L.LB[v] : L.S[v];
+  if constexpr (FIN) {
+    const bool e = (t == L.tmax);
+#pragma unroll
+    for (int v = 0; v < 3; ++v) L.fin[v] = e ? L.S[v] : L.fin[v];
+  }
+  const bool fr = (t == L.tmax + 1);
+  L.S[0] = fr ? MSA_NEG : L.S[0];
+  L.S[2] = fr ? MSA_NEG : L.S[2];
+  carry[0] = L.S[0];
+  carry[1] = L.S[2];
+}
+
 // Bounded spin helper for cross-workgroup granule waits.
 __device__ __forceinline__ unsigned long long gload(const unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -941,7 +973,13 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
             int cr[3];
             int ct = gdiag + kp.gap_open * t;
             if constexpr (swlin(ALG)) asm("" : "+s"(ct));  // one SGPR feeds both the floor and H
-            const unsigned d = step<ALG, OUT, MASKED, TRACKPOS, FIN>(kp, L, inv, s, t, ct, cr, hv[k]);
+            unsigned d;
+            if constexpr (ALG == MSA_ALG_NWA && MASKED) {
+              d = step<ALG, OUT, false, TRACKPOS, false>(kp, L, inv, s, t, ct, cr, hv[k]);
+              band_fix<FIN>(L, t, cr);
+            } else {
+              d = step<ALG, OUT, MASKED, TRACKPOS, FIN>(kp, L, inv, s, t, ct, cr, hv[k]);
+            }
 #pragma unroll
             for (int v = 0; v < NC; ++v) hist[v][k] = cr[v];
             if constexpr (SHREG) shreg = dpp_shl1(cr[0], shreg);
