@@ -173,7 +173,7 @@ typedef void (*kfn_t)(KArgs);
 // two or three values per cell are carried (register pressure: no spills)
 constexpr int ks_single(int alg) { return (alg == MSA_ALG_SWL || alg == MSA_ALG_SWL0) ? MSA_KS_SINGLE : 16; }
 
-template <int ALG, int OUT, bool TP>
+template <int ALG, int OUT, int TP>
 kfn_t kf(bool sgl) {
   // single pair: (MSA_WAVES_SINGLE waves, MSA_KS_SINGLE steps/phase); batch: (MSA_WAVES_BATCH, MSA_KS_BATCH)
   return sgl ? stripe_kernel<ALG, OUT, TP, MSA_WAVES_SINGLE, ks_single(ALG), true>
@@ -181,7 +181,7 @@ kfn_t kf(bool sgl) {
 }
 
 kfn_t pick_kernel(int alg, int out, int tp, bool sgl) {
-#define K3(A, O) return tp ? kf<A, O, true>(sgl) : kf<A, O, false>(sgl)
+#define K3(A, O) return tp == 2 ? kf<A, O, 2>(sgl) : (tp ? kf<A, O, 1>(sgl) : kf<A, O, 0>(sgl))
   switch (alg) {
     case MSA_ALG_SWL:
       if (out == MSA_OUT_NONE) K3(MSA_ALG_SWL, MSA_OUT_NONE);
@@ -197,17 +197,17 @@ kfn_t pick_kernel(int alg, int out, int tp, bool sgl) {
       if (out == MSA_OUT_DIR) K3(MSA_ALG_SWA, MSA_OUT_DIR);
       break;
     case MSA_ALG_NWA:
-      if (out == MSA_OUT_NONE) return kf<MSA_ALG_NWA, MSA_OUT_NONE, false>(sgl);
-      if (out == MSA_OUT_H) return kf<MSA_ALG_NWA, MSA_OUT_H, false>(sgl);
+      if (out == MSA_OUT_NONE) return kf<MSA_ALG_NWA, MSA_OUT_NONE, 0>(sgl);
+      if (out == MSA_OUT_H) return kf<MSA_ALG_NWA, MSA_OUT_H, 0>(sgl);
       break;
     case MSA_ALG_REF:
-      if (out == MSA_OUT_NONE) return kf<MSA_ALG_REF, MSA_OUT_NONE, false>(sgl);
-      if (out == MSA_OUT_TAB) return kf<MSA_ALG_REF, MSA_OUT_TAB, false>(sgl);
-      if (out == MSA_OUT_DIR) return kf<MSA_ALG_REF, MSA_OUT_DIR, false>(sgl);
-      if (out == MSA_OUT_H) return kf<MSA_ALG_REF, MSA_OUT_H, false>(sgl);
+      if (out == MSA_OUT_NONE) return kf<MSA_ALG_REF, MSA_OUT_NONE, 0>(sgl);
+      if (out == MSA_OUT_TAB) return kf<MSA_ALG_REF, MSA_OUT_TAB, 0>(sgl);
+      if (out == MSA_OUT_DIR) return kf<MSA_ALG_REF, MSA_OUT_DIR, 0>(sgl);
+      if (out == MSA_OUT_H) return kf<MSA_ALG_REF, MSA_OUT_H, 0>(sgl);
       break;
     case MSA_ALG_PART:
-      if (out == MSA_OUT_TAB) return kf<MSA_ALG_PART, MSA_OUT_TAB, false>(sgl);
+      if (out == MSA_OUT_TAB) return kf<MSA_ALG_PART, MSA_OUT_TAB, 0>(sgl);
       break;
   }
 #undef K3
@@ -357,7 +357,15 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     case MSA_PARTIAL: kalg = MSA_ALG_PART; break;
     default: delete P; return MSA_ERR_ARG;
   }
-  const int tp = (kalg == MSA_ALG_SWL || kalg == MSA_ALG_SWL0 || kalg == MSA_ALG_SWA) ? (desc->track_end ? 1 : 0) : 0;
+  int tp = (kalg == MSA_ALG_SWL || kalg == MSA_ALG_SWL0 || kalg == MSA_ALG_SWA) ? (desc->track_end ? 1 : 0) : 0;
+  if (tp) {
+    // the first-maximum position packs with the value into one int (TRACKPOS 2) when every
+    // local score is below 2^16 (H <= match * min(m, n)) and a stripe has < 2^15 steps
+    bool pack = true;
+    for (int64_t p = 0; p < desc->n_pairs && pack; ++p)
+      pack = (int64_t)std::max(0, desc->match) * std::min(desc->m[p], desc->n[p]) < 65536 && desc->n[p] + 512 < 32768;
+    if (pack) tp = 2;
+  }
   if (desc->single && desc->n_pairs != 1) { delete P; return MSA_ERR_ARG; }
   // A banded pair has only ~(2*band+64)/(64*lag) stripes in flight at once:
   // one workgroup cycling its waves over all stripes (the batch kernel, wrap

@@ -239,7 +239,11 @@ struct LaneState {
 // (the 2g is folded into the substitution profile), so the loop-carried chain
 // per step is DPP -> v_max3 instead of DPP -> max -> sub -> max3.  Rings and
 // granules carry G; H = G - g*(i+j) is only formed for the output / best.
-template <int ALG, int OUT, bool MASKED, bool TRACKPOS, bool FIN = false>
+// TRACKPOS: 0 = best value only, 1 = best value and its first step, 2 = the same as one
+// packed int (value << 15 | 32767 - step; plans with H < 2^16 and < 2^15 steps per
+// stripe): one max instead of a compare and two selects per step, and a larger key is
+// the larger value, then the earlier step -- the first maximum, as in mode 1.
+template <int ALG, int OUT, bool MASKED, int TRACKPOS, bool FIN = false>
 __device__ __forceinline__ unsigned step(const msa_kparams& kp, LaneState<ALG>& L, const int (&in)[3], int s,
                                          int t, int ct, int (&carry)[3], int& hout) {
   unsigned dir = 0;
@@ -332,7 +336,9 @@ __device__ __forceinline__ unsigned step(const msa_kparams& kp, LaneState<ALG>& 
     if constexpr (swlin(ALG) || ALG == MSA_ALG_SWA) {
       const int hv = swlin(ALG) ? nS[0] - ct : nS[0];
       hout = hv;
-      if (!before && !after) {
+      if constexpr (TRACKPOS == 2) {
+        L.best = imax(L.best, (!before && !after) ? (hv << 15) + (32767 - t) : 0);
+      } else if (!before && !after) {
         if constexpr (TRACKPOS) {
           if (hv > L.best) { L.best = hv; L.bt = t; }
         } else {
@@ -349,7 +355,9 @@ __device__ __forceinline__ unsigned step(const msa_kparams& kp, LaneState<ALG>& 
     if constexpr (swlin(ALG) || ALG == MSA_ALG_SWA) {
       const int hv = swlin(ALG) ? nS[0] - ct : nS[0];
       hout = hv;
-      if constexpr (TRACKPOS) {
+      if constexpr (TRACKPOS == 2) {
+        L.best = imax(L.best, (hv << 15) + (32767 - t));
+      } else if constexpr (TRACKPOS) {
         if (hv > L.best) { L.best = hv; L.bt = t; }
       } else {
         L.best = imax(L.best, hv);
@@ -493,7 +501,7 @@ __device__ __forceinline__ unsigned long long loader_issue(const KArgs& a, int c
 }
 
 // SGL: single-pair variant (loader + code wave, LDS code ring, DPP shift-register hand-off)
-template <int ALG, int OUT, bool TRACKPOS, int W, int KS, bool SGL>
+template <int ALG, int OUT, int TRACKPOS, int W, int KS, bool SGL>
 __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KArgs a) {
   static_assert(KS % 16 == 0 && KS <= 64, "phases are whole 16-step layout blocks");
   constexpr int CPP = KS / 16;  // 16-column chunks per phase
@@ -1080,9 +1088,11 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
       msa_stripe_meta* md = a.meta + pd.stripe0 + ks;
       if constexpr (swlin(ALG) || ALG == MSA_ALG_SWA) {
         // first max in row-major order: max best, then min row
-        int b = (L.i <= m) ? L.best : INT32_MIN;
+        const int bv = (TRACKPOS == 2) ? (L.best >> 15) : L.best;
+        const int bt = (TRACKPOS == 2) ? 32767 - (L.best & 32767) : L.bt;
+        int b = (L.i <= m) ? bv : INT32_MIN;
         int bi = L.i;
-        int bj = sg.cs + L.bt - lane;
+        int bj = sg.cs + bt - lane;
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) {
           const int ob = __shfl_xor(b, off);
