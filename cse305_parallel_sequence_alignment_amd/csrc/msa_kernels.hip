@@ -910,8 +910,13 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
       unsigned long long* const g_out = a.gbuf + (size_t)group * NC * a.gbuf_stride;
       const size_t obase = (size_t)pd.out_off + (size_t)ks * pd.pmax * MSA_K * 64;  // pmax: 16-step blocks
 
+      // MASKED_: 0 no range checks; 1 per-lane start/end checks; 2..5 banded Gotoh in the
+      // regular middle of the band, head (2, 3) or tail (4, 5) fix-ups by v_writelane, fix-up
+      // steps of parity MODE & 1 (see band_fix / the range split below)
+      int fix_base = 0;  // lane fixed up at the phase's first fix-up step (modes 2..5)
       auto run_phase = [&](const int q, auto MASKED_, auto INMASK_, auto FIN_) __attribute__((always_inline)) {
-        constexpr bool MASKED = decltype(MASKED_)::value;  // per-lane start/end checks
+        constexpr int MMODE = (int)decltype(MASKED_)::value;
+        constexpr bool MASKED = MMODE != 0;
         constexpr bool INMASK = decltype(INMASK_)::value;  // input columns beyond the producer's last
         constexpr bool FIN = decltype(FIN_)::value;        // capture the state at each row's last column
         // ---- all LDS reads of the phase up front (one exposed latency per phase) ----
@@ -982,7 +987,26 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
             int ct = gdiag + kp.gap_open * t;
             if constexpr (swlin(ALG)) asm("" : "+s"(ct));  // one SGPR feeds both the floor and H
             unsigned d;
-            if constexpr (ALG == MSA_ALG_NWA && MASKED) {
+            if constexpr (ALG == MSA_ALG_NWA && MMODE >= 2) {
+              d = step<ALG, OUT, false, TRACKPOS, false>(kp, L, inv, s, t, ct, cr, hv[k]);
+              // one lane per two steps sits on the band's edge: its index is wave-uniform
+              constexpr int PAR = MMODE & 1;
+              if (((k - PAR) & 1) == 0) {
+                const int rr = fix_base + ((k - PAR) >> 1);
+                // the lane select goes through M0 (one SGPR source per VALU op: the value is
+                // the other); s_nop 3 covers the SALU-write -> lane-select wait states
+                const int negv = MSA_NEG;
+                if constexpr (MMODE <= 3) {  // head: the row's left neighbour is -inf
+                  asm("s_mov_b32 m0, %3\n\ts_nop 3\n\tv_writelane_b32 %0, %2, m0\n\tv_writelane_b32 %1, %2, m0"
+                      : "+v"(L.S[0]), "+v"(L.S[1]) : "s"(negv), "s"(rr) : "m0");
+                } else {  // tail: the row below's (and the hand-off's) up value is -inf
+                  asm("s_mov_b32 m0, %3\n\ts_nop 3\n\tv_writelane_b32 %0, %2, m0\n\tv_writelane_b32 %1, %2, m0"
+                      : "+v"(L.S[0]), "+v"(L.S[2]) : "s"(negv), "s"(rr) : "m0");
+                  cr[0] = L.S[0];
+                  cr[1] = L.S[2];
+                }
+              }
+            } else if constexpr (ALG == MSA_ALG_NWA && MASKED) {
               d = step<ALG, OUT, false, TRACKPOS, false>(kp, L, inv, s, t, ct, cr, hv[k]);
               band_fix<FIN>(L, t, cr);
             } else {
@@ -1079,9 +1103,51 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
         run_range(qa, qb, F_{}, F_{}, F_{});
         run_range(qb, P, T_{}, T_{}, T_{});
       } else {
-        run_range(0, qa, T_{}, T_{}, F_{});
-        run_range(qa, qb, F_{}, F_{}, F_{});
-        run_range(qb, P, T_{}, T_{}, F_{});
+        // banded Gotoh, a full stripe away from the matrix borders: lane r's first step is
+        // A0 + 2r and its last C0 + 2r, so at a step of the right parity exactly one lane
+        // needs the head (or tail) fix-up, at an index the wave knows in a scalar register.
+        // Phases whose every fix-up lane is in [0, 63] take the v_writelane path (2 lane
+        // writes per two steps instead of 2 compares and 5 selects per step); the others,
+        // and every other stripe, band_fix.
+        bool regular = false;
+        int A0 = 0, C0 = 0;
+        if constexpr (ALG == MSA_ALG_NWA) {
+          const int i0 = 64 * ks + 1;
+          regular = uni(kp.band >= 64 && i0 + 63 <= m && i0 - kp.band > 1 && i0 + 63 + kp.band < n);
+          A0 = uni(jlo_of(i0, kp.band) - sg.cs);
+          C0 = uni(jhi_of(i0, n, kp.band) - sg.cs);
+        }
+        if (regular) {
+          const int par = (A0 - 1) & 1;
+          const int h0 = min(qa, max(0, (A0 - 1 + 15) / 16));
+          const int h1 = min(qa, max(h0, (A0 + 110) / 16 + 1));
+          const int t0 = min(P, max(qb, (C0 + 1 + 15) / 16));
+          const int t1 = min(P, max(t0, (C0 + 112) / 16 + 1));
+          using H0 = std::integral_constant<int, 2>;
+          using H1 = std::integral_constant<int, 3>;
+          using E0 = std::integral_constant<int, 4>;
+          using E1 = std::integral_constant<int, 5>;
+          // fix_base: lane of the phase's first fix-up step, (16q + par - (A0 - 1)) / 2 (head)
+          // or (16q + par - (C0 + 1)) / 2 (tail)
+          auto run_fast = [&](const int qb_, const int qe_, auto MODE_, const int edge) __attribute__((always_inline)) {
+            for (int q = qb_; q < qe_; ++q) {
+              fix_base = uni((KS * q + par - edge) >> 1);
+              run_phase(q, MODE_, T_{}, F_{});
+              MSA_SYNC(ph + q);
+            }
+          };
+          run_range(0, h0, T_{}, T_{}, F_{});
+          if (par) run_fast(h0, h1, H1{}, A0 - 1); else run_fast(h0, h1, H0{}, A0 - 1);
+          run_range(h1, qa, T_{}, T_{}, F_{});
+          run_range(qa, qb, F_{}, F_{}, F_{});
+          run_range(qb, t0, T_{}, T_{}, F_{});
+          if (par) run_fast(t0, t1, E1{}, C0 + 1); else run_fast(t0, t1, E0{}, C0 + 1);
+          run_range(t1, P, T_{}, T_{}, F_{});
+        } else {
+          run_range(0, qa, T_{}, T_{}, F_{});
+          run_range(qa, qb, F_{}, F_{}, F_{});
+          run_range(qb, P, T_{}, T_{}, F_{});
+        }
       }
       ph += P;
       // ---- stripe finalize ----
