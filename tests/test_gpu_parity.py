@@ -246,6 +246,45 @@ def test_sw_affine_traceback(oracle, dev):
             assert (r["score"], r["end"], r["beg"], r["cigar"]) == (o["score"], o["end"], o["beg"], o["cigar"])
 
 
+@pytest.mark.parametrize("alg,m,n,ma,mi,go,ge", [
+    ("affine", 2100, 2000, 40, -30, 50, 10),   # score bound 40 x 2000 >= 2^16: unpacked tracking
+    ("affine", 700, 800, 1, 0, 3, 1),          # packed (value << 15 | 32767 - step)
+    ("linear", 1900, 2100, 40, -25, 30, 30),   # unpacked, SW linear
+    ("linear", 900, 1000, 2, -1, 1, 1),        # packed, SW linear
+])
+def test_first_maximum_tracking_modes(oracle, dev, LB, alg, m, n, ma, mi, go, ge):
+    """track_end plans pick the packed first-maximum mode when every score is below 2^16 and a stripe has
+    fewer than 2^15 steps, else the compare-and-select mode: both must report the oracle's score and its
+    first (row-major) end cell, and the affine plans' device traceback the oracle's CIGAR."""
+    import torch
+    from cse305_parallel_sequence_alignment_amd.plan import Plan, cigar_of
+
+    rng = np.random.default_rng(m + n + ma)
+    A, B = rs(rng, m), rs(rng, n)
+    B = A[100:1100] + B[1000:]  # a long local match, so high-scoring alignments exist
+    n = len(B)
+    if alg == "affine":
+        pl = Plan(LB.SW_AFFINE, LB.CELLS_DIR, [m], [n], [0], [0], match=ma, mismatch=mi, gap_open=go,
+                  gap_extend=ge, track_end=True)
+        out = torch.empty(pl.cells_elems, dtype=torch.uint8, device=dev)
+    else:
+        pl = Plan(LB.SW_LINEAR, LB.CELLS_H, [m], [n], [0], [0], match=ma, mismatch=mi, gap_open=go,
+                  gap_extend=ge, track_end=True)
+        out = torch.empty(pl.cells_elems, dtype=torch.int32, device=dev)
+    pl.run(_dev(A, dev), _dev(B, dev), out)
+    r = pl.results()[0]
+    o = oracle.sw(A, B, ma, mi, go, ge, want_tb=(alg == "affine"))
+    assert (r["score"], tuple(r["end"])) == (o["score"], tuple(o["end"]))
+    if alg == "affine":
+        ops = torch.empty(m + n + 2, dtype=torch.uint8, device=dev)
+        info = torch.zeros(8, dtype=torch.int64, device=dev)
+        pl.traceback_async(out, ops, info)
+        inf = info.cpu().tolist()
+        assert inf[3] == 0
+        assert cigar_of(bytes(ops[:inf[0]].cpu().numpy().tobytes())) == o["cigar"]
+        assert (inf[1], inf[2]) == tuple(o["beg"])
+
+
 @pytest.mark.parametrize("track_end", [False, True])
 def test_sw_linear_10k_c2(oracle, dev, LB, track_end):
     """C2 exactly as bench.py runs it (data.c2_pair, match 1 / mismatch 0 / gap 1, H written; track_end=False
