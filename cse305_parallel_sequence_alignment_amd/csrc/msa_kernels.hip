@@ -994,14 +994,19 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
               if (((k - PAR) & 1) == 0) {
                 const int rr = fix_base + ((k - PAR) >> 1);
                 // the lane select goes through M0 (one SGPR source per VALU op: the value is
-                // the other); s_nop 3 covers the SALU-write -> lane-select wait states
+                // the other), saved and restored around the writes (M0 is reserved to the
+                // compiler); s_nop 3 covers the SALU-write -> lane-select wait states
                 const int negv = MSA_NEG;
                 if constexpr (MMODE <= 3) {  // head: the row's left neighbour is -inf
-                  asm("s_mov_b32 m0, %3\n\ts_nop 3\n\tv_writelane_b32 %0, %2, m0\n\tv_writelane_b32 %1, %2, m0"
-                      : "+v"(L.S[0]), "+v"(L.S[1]) : "s"(negv), "s"(rr) : "m0");
+                  int keep;
+                  asm("s_mov_b32 %2, m0\n\ts_mov_b32 m0, %4\n\ts_nop 3\n\tv_writelane_b32 %0, %3, m0\n\t"
+                      "v_writelane_b32 %1, %3, m0\n\ts_mov_b32 m0, %2"
+                      : "+v"(L.S[0]), "+v"(L.S[1]), "=&s"(keep) : "s"(negv), "s"(rr));
                 } else {  // tail: the row below's (and the hand-off's) up value is -inf
-                  asm("s_mov_b32 m0, %3\n\ts_nop 3\n\tv_writelane_b32 %0, %2, m0\n\tv_writelane_b32 %1, %2, m0"
-                      : "+v"(L.S[0]), "+v"(L.S[2]) : "s"(negv), "s"(rr) : "m0");
+                  int keep;
+                  asm("s_mov_b32 %2, m0\n\ts_mov_b32 m0, %4\n\ts_nop 3\n\tv_writelane_b32 %0, %3, m0\n\t"
+                      "v_writelane_b32 %1, %3, m0\n\ts_mov_b32 m0, %2"
+                      : "+v"(L.S[0]), "+v"(L.S[2]), "=&s"(keep) : "s"(negv), "s"(rr));
                   cr[0] = L.S[0];
                   cr[1] = L.S[2];
                 }
