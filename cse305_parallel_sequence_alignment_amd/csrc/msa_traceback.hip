@@ -137,6 +137,9 @@ __global__ __launch_bounds__(64) void sw_traceback_kernel(const uint8_t* __restr
       if (4 * g + q < pmax) glds16(base + (blk0 + q) * 1024, dst + 1024u * q);
   };
   int n_switch = 0, n_sync = 0;               // group switches, of them fetched on demand
+#ifdef MSA_TB_STATS
+  long long n_outer = 0, n_win = 0, t_win = 0;  // diagnostic build: outer iterations, windows, ticks in windows
+#endif
   long long t_wait = 0;                        // clock ticks spent waiting for group loads
   const long long t_begin = (long long)__builtin_amdgcn_s_memtime();
   auto timed_wait = [&]() {
@@ -213,6 +216,10 @@ __global__ __launch_bounds__(64) void sw_traceback_kernel(const uint8_t* __restr
       // inside the 8 x 8 window, the budget keeps them inside the group.
       const int wa = lane >> 3, wb = lane & 7;
       bool stop = false;
+#ifdef MSA_TB_STATS
+      ++n_outer;
+      const long long tw0 = (long long)__builtin_amdgcn_s_memtime();
+#endif
       int sh = 9 * st;
       while (budget > 0 && !stop) {
         const int kmax = budget < 7 ? budget : 7;
@@ -225,13 +232,29 @@ __global__ __launch_bounds__(64) void sw_traceback_kernel(const uint8_t* __restr
         const int wt = (int)(fH | (fE << 9) | (fF << 18));
         int idx = 0, k = 0;
         unsigned wcode = 0;
-        for (; k < kmax; ++k) {
-          const unsigned f = (unsigned)__builtin_amdgcn_readlane(wt, idx) >> sh;
-          const unsigned dl = f & 15u;
-          sh = (int)((f >> 4) & 31u);
-          idx += (int)dl;
-          wcode |= dl << (4 * k);
-          if (sh == 27) { ++k; stop = true; break; }
+        if (kmax == 7) {
+          // a full window (the common case), unrolled: per step a v_readlane and five scalar
+          // ops, and a stop test that is taken once per traceback (the runtime-bounded loop
+          // below compiles to ~25 scalar instructions and two branches per step)
+#pragma unroll
+          for (int kk = 0; kk < 7; ++kk) {
+            const unsigned f = (unsigned)__builtin_amdgcn_readlane(wt, idx) >> sh;
+            const unsigned dl = f & 15u;
+            sh = (int)((f >> 4) & 31u);
+            idx += (int)dl;
+            wcode |= dl << (4 * kk);
+            k = kk + 1;
+            if (sh == 27) { stop = true; break; }
+          }
+        } else {
+          for (; k < kmax; ++k) {
+            const unsigned f = (unsigned)__builtin_amdgcn_readlane(wt, idx) >> sh;
+            const unsigned dl = f & 15u;
+            sh = (int)((f >> 4) & 31u);
+            idx += (int)dl;
+            wcode |= dl << (4 * k);
+            if (sh == 27) { ++k; stop = true; break; }
+          }
         }
         rawl[nw] = wcode | ((unsigned)k << 28);  // every lane stores the same word
         if (++nw == TB_RAW) decode();
@@ -239,7 +262,13 @@ __global__ __launch_bounds__(64) void sw_traceback_kernel(const uint8_t* __restr
         r -= da;
         t -= da + db;
         budget -= k;
+#ifdef MSA_TB_STATS
+        ++n_win;
+#endif
       }
+#ifdef MSA_TB_STATS
+      t_win += (long long)__builtin_amdgcn_s_memtime() - tw0;
+#endif
       st = stop ? 3 : sh / 9;
       i -= r_in - r;                  // rows consumed
       j -= (t_in - t) - (r_in - r);   // columns consumed
@@ -259,8 +288,15 @@ __global__ __launch_bounds__(64) void sw_traceback_kernel(const uint8_t* __restr
     info[3] = status;
     info[4] = n_switch;
     info[5] = n_sync;
+#ifdef MSA_TB_STATS
+    info[3] = n_outer;
+    info[5] = n_win;
+    info[7] = t_win;
+#endif
     info[6] = (long long)__builtin_amdgcn_s_memtime() - t_begin;  // s_memtime ticks, whole walk
+#ifndef MSA_TB_STATS
     info[7] = t_wait;
+#endif
   }
 }
 
