@@ -66,7 +66,8 @@ def cpu_baseline(wl: str, A: bytes, B: bytes, cores: int):
     horizontal gap: oracle/cpu_rowsweep.cpp) on this host, p' = 1 and p' = cores, bounded samples."""
     from oracle import oracle as O
 
-    mode = 0 if wl == "c3" else 1  # c3: the reference's own Gotoh recurrence; else SW linear int32
+    # c3 / c5 (affine gaps): the reference's own Gotoh recurrence; c2 / c4: SW linear int32
+    mode = 0 if wl in ("c3", "c5") else 1
     L = min(len(A), len(B), 10000)
     A, B = A[:L], B[:L]
     pts = []
