@@ -225,7 +225,12 @@ __global__ __launch_bounds__(64) void sw_traceback_kernel(const uint8_t* __restr
         const int kmax = budget < 7 ? budget : 7;
         const int rr = r - wa, tt = t - wa - wb;
         const bool in_grp = rr >= 0 && (tt >> 6) == (t >> 6);
-        const unsigned dv = in_grp ? (unsigned)grp[(((tt >> 4) & 3) << 10) | (rr << 4) | (tt & 15)] : 0u;
+        // every lane reads (a clamped address when its cell is outside the group): no
+        // exec-mask branch around the LDS read
+        const int ga = in_grp ? ((((tt >> 4) & 3) << 10) | (rr << 4) | (tt & 15)) : 0;
+        unsigned raw = grp[ga];
+        asm("" : "+v"(raw));  // keep the read unconditional
+        const unsigned dv = in_grp ? raw : 0u;
         const unsigned fH = (unsigned)(TB_FH >> (16 * (dv & 3u))) & 0x1ffu;
         const unsigned fE = 1u | ((dv & 4u) ? 0u : (9u << 4));
         const unsigned fF = 8u | ((dv & 8u) ? 0u : (18u << 4));
