@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Benchmark of the hot path (BASELINE.json metric: GCUPS, 10k x 10k Smith-Waterman).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c4|c3|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c4|c3|c5|ref] [--ref-len L]
 
 One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI when
 launched by torch.distributed.run).  A "step" is one pass of the DP fill over
@@ -18,6 +18,12 @@ one batch of input already resident in HBM:
 * c5: one 20k x 20k affine SW fill writing 1 B/cell traceback bits, then the
   traceback on the device (one wave walks the bits from the end cell): a step
   is fill + traceback.
+* ref: the reference's own boundary, main_alignment_function (global Gotoh,
+  g=1 h=2, start/end type -1) on seq0 x seq1 at --ref-len (10k default, 20k):
+  a step is the fill writing 1 B/cell direction bytes + find_alignment's walk
+  on the device, inputs resident in HBM.  The whole C-ABI call (host buffers
+  in, printed text out: PCIe, plan set-up, node list and print_seq included)
+  is timed separately and reported as boundary_call_ms, never as the value.
 
 After the timed steps (outside the timed region) the run is checked: the
 plan's sticky error word must be 0 (every timed step completed its waits), the
@@ -47,7 +53,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s (spec)
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # = 78.64 T int32 lane-ops/s
 # algorithmic bytes / ops per cell, fixed up front
 BYTES_PER_CELL = {"c2": 4.0, "c3": 4.0}
-OPS_PER_CELL = {"c4": 8.0, "c5": 12.0}
+OPS_PER_CELL = {"c4": 8.0, "c5": 12.0, "ref": 13.0}  # ref: T1 add + 2 max, T2 / T3 3 sub + 2 max each
 
 
 def parse():
@@ -55,7 +61,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2", choices=["c2", "c4", "c3", "c5"])
+    ap.add_argument("--workload", default="c2", choices=["c2", "c4", "c3", "c5", "ref"])
+    ap.add_argument("--ref-len", type=int, default=10000, help="ref workload: seq0 x seq1 prefix length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--synthetic", action="store_true", help="i.i.d. ACGT (splitmix seed) instead of the dataset")
     return ap.parse_args()
@@ -66,12 +73,13 @@ def cpu_baseline(wl: str, A: bytes, B: bytes, cores: int):
     horizontal gap: oracle/cpu_rowsweep.cpp) on this host, p' = 1 and p' = cores, bounded samples."""
     from oracle import oracle as O
 
-    # c3 / c5 (affine gaps): the reference's own Gotoh recurrence; c2 / c4: SW linear int32
-    mode = 0 if wl in ("c3", "c5") else 1
+    # c3 / c5 / ref (affine gaps): the reference's own Gotoh recurrence; c2 / c4: SW linear int32
+    mode = 0 if wl in ("c3", "c5", "ref") else 1
     L = min(len(A), len(B), 10000)
     A, B = A[:L], B[:L]
     pts = []
-    for p, rows in ((1, L), (cores, min(L, 1500))):
+    # ref: p' = 11 is what the reference's harness runs (main_alignment_function(..., p=32): p' = (p+2)/3)
+    for p, rows in ((1, L), ((11 if wl == "ref" else cores), min(L, 1500))):
         _, secs = O.rowsweep(A, B, p=p, mode=mode, g=1.0, h=2.0, match=1, mismatch=0, rows=rows)
         pts.append(dict(threads=p, rows=rows, cols=L, seconds=round(secs, 3), gcups=round(rows * L / secs / 1e9, 4)))
     best = max(pts, key=lambda x: x["gcups"])
@@ -142,6 +150,16 @@ def main():
         cells_per_step = m * n
         desc = ("sw-affine 20000x20000, open 3 extend 1, 1 B/cell traceback bits written + traceback on the "
                 "device (ops + begin cell)")
+    elif wl == "ref":
+        L = args.ref_len
+        A, B = data.bundled()[0][:L], data.bundled()[1][:L]
+        m, n = len(A), len(B)
+        pairs_m, pairs_n, a_off, b_off = [m], [n], [0], [0]
+        plan_kw = dict(alg=LB.REF_GOTOH, cells=LB.CELLS_DIR, match=1, mismatch=0, gap_open=3, gap_extend=1,
+                       start_type=-1)
+        cells_per_step = m * n
+        desc = (f"main_alignment_function's path: reference Gotoh {m}x{n} (seq0 x seq1, g=1 h=2, start/end type -1), "
+                f"1 B/cell direction bytes + find_alignment's walk on the device")
     else:  # c4
         total = data.C4_PAIRS
         L = data.C4_LEN
@@ -186,6 +204,13 @@ def main():
         def step():
             plan.run(dA, dB, out)
             plan.traceback_async(out, tb_ops, tb_info)  # same stream: walks the bits this run wrote
+    elif wl == "ref":
+        tb_ops = torch.empty(m + n + 2, dtype=torch.uint8, device=dev)
+        tb_info = torch.zeros(8, dtype=torch.int64, device=dev)
+
+        def step():
+            plan.run(dA, dB, out)
+            plan.traceback_gotoh_async(out, tb_ops, tb_info, -1)  # find_alignment's walk, same stream
     else:
         def step():
             plan.run(dA, dB, out)
@@ -236,6 +261,29 @@ def main():
                                                    (inf[1], inf[2]) == tuple(o["beg"]))
     elif wl == "c3":
         checks["score_matches_cpu"] = bool(int(O.banded_ref(A, B, 512, 1.0, 2.0)) == res[0]["score"])
+    elif wl == "ref":
+        import hashlib
+
+        from cse305_parallel_sequence_alignment_amd import api
+
+        inf = tb_info.cpu().tolist()
+        fx = [c for c in json.loads((REPO / "tests" / "golden" / "at_size.json").read_text())
+              if (c["a"], c["b"], c["L"], c["g"], c["h"]) == (0, 1, m, 1.0, 2.0)]
+        # the boundary call itself (host buffers in, text out), timed outside the device-resident steps
+        tb0 = time.perf_counter()
+        for _ in range(3):
+            text, sc = api.main_alignment_text(b"\0" + A, b"\0" + B, m, n, 32, 1.0, 2.0)
+        boundary_ms = (time.perf_counter() - tb0) / 3 * 1e3
+        lines = text.split("\n")[5:7]
+        checks["walk_status_ok"] = bool(inf[3] == 0 and min(inf[1], inf[2]) == 1)
+        if fx:  # the reference's own outputs at this size (make_golden.py at_size)
+            checks["score_matches_reference"] = bool(sc == fx[0]["score"] == max(res[0]["fin"]))
+            checks["text_matches_reference"] = bool(
+                hashlib.md5((lines[0] + "\n" + lines[1] + "\n").encode()).hexdigest() == fx[0]["lines_md5"] and
+                len(lines[0]) == fx[0]["n_nodes"] == inf[0])
+        else:
+            o = O.main_alignment_text(A, B, 1.0, 2.0)
+            checks["text_matches_cpu"] = bool(text == o[0])
     else:
         got = [int(x) for x in gathered.cpu().tolist()]
         fx = REPO / "tests" / "golden" / "c4_scores.json"
@@ -255,11 +303,14 @@ def main():
         kms.append(plan.kernel_ms())
     kern_ms = float(np.mean(kms))
     tb_ms = None
-    if wl == "c5":  # the device traceback alone (torch events: it runs on torch's current stream)
+    if wl in ("c5", "ref"):  # the device traceback alone (torch events: it runs on torch's current stream)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(5):
-            plan.traceback_async(out, tb_ops, tb_info)
+            if wl == "c5":
+                plan.traceback_async(out, tb_ops, tb_info)
+            else:
+                plan.traceback_gotoh_async(out, tb_ops, tb_info, -1)
         e1.record()
         torch.cuda.synchronize()
         tb_ms = e0.elapsed_time(e1) / 5
@@ -315,7 +366,11 @@ def main():
                            score_rank0=int(res[0]["score"]), checks_all_ranks=bool(ok.item()), **checks,
                            kernel_errors=0, dp_kernel_ms=round(kern_ms, 4),
                            **({"traceback_ms": round(tb_ms, 4), "traceback_walk": tb_walk} if tb_ms is not None
-                              else {})),
+                              else {}),
+                           **({"boundary_call_ms": round(boundary_ms, 3),
+                               "boundary_note": "msa_main_alignment with host buffers (plan set-up, H2D codes, fill, "
+                                                "device walk, D2H ops, node list, print_seq text): PCIe-inclusive, "
+                                                "not the value"} if wl == "ref" else {})),
             "roofline": roof,
             "cpu_baseline": cpu,
         }

@@ -105,6 +105,7 @@ def lib() -> C.CDLL:
     L.msa_plan_pair_layout.argtypes = [P, i64, C.POINTER(i64)]
     L.msa_plan_checksum.argtypes = [P, P, i64, C.POINTER(u64), P]
     L.msa_plan_traceback.argtypes = [P, i64, P, P, i64, P, P]
+    L.msa_plan_traceback_gotoh.argtypes = [P, i64, C.c_int, P, P, i64, P, P]
     L.msa_plan_last_kernel_ms.argtypes = [P, C.POINTER(C.c_float)]
     L.msa_plan_set_timing.argtypes = [P, i32]
     L.msa_encode_pair.argtypes = [P, sz, P, sz, P, P]
@@ -132,6 +133,6 @@ EXPORTED = [
     "msa_partial_partition", "msa_partial_tables", "msa_plan_create", "msa_plan_destroy", "msa_plan_cells_size",
     "msa_plan_run", "msa_plan_results", "msa_plan_error", "msa_plan_clear_error", "msa_plan_scores",
     "msa_plan_stripe_meta", "msa_plan_stripes", "msa_plan_pair_layout",
-    "msa_plan_checksum", "msa_plan_traceback",
+    "msa_plan_checksum", "msa_plan_traceback", "msa_plan_traceback_gotoh",
     "msa_plan_last_kernel_ms", "msa_plan_set_timing", "msa_encode_pair", "msa_sw_align",
 ]

@@ -59,14 +59,22 @@ int ensure_device() {
   return g_dev_ok ? MSA_OK : MSA_ERR_NODEV;
 }
 
+int current_device() {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  return dev;
+}
+
 // Device memory pool.  The reference's harness calls main_alignment_function
 // from hardware_concurrency threads at once (testing.cpp:145-158, 269-280,
 // 352-358); with plain hipMalloc/hipFree every call would serialize on
-// hipFree's implicit device synchronization.  Blocks are cached per size class
-// (powers of two up to 1 MiB, then 2 MiB multiples) in one mutex-protected
-// free list; a block is only returned by its owner after the stream work that
-// used it has completed (run_one syncs its stream, msa_plan_destroy syncs the
-// plan's last stream), so a block never changes hands while a kernel uses it.
+// hipFree's implicit device synchronization.  Blocks are cached per (device,
+// size class) (powers of two up to 1 MiB, then 2 MiB multiples) in one
+// mutex-protected free list, so a block allocated while device d was current
+// is only handed to a caller for which d is current.  A block is only returned
+// by its owner after the stream work that used it has completed (run_one syncs
+// its stream, msa_plan_destroy syncs every stream the plan queued work on), so
+// a block never changes hands while a kernel uses it.
 class DevPool {
  public:
   static size_t size_class(size_t b) {
@@ -81,9 +89,10 @@ class DevPool {
   }
   void* get(size_t bytes) {
     const size_t c = size_class(bytes);
+    const int dev = current_device();
     {
       std::lock_guard<std::mutex> lk(mu_);
-      auto it = free_.find(c);
+      auto it = free_.find(std::make_pair(dev, c));
       if (it != free_.end()) {
         void* p = it->second;
         free_.erase(it);
@@ -92,7 +101,18 @@ class DevPool {
       }
     }
     void* p = nullptr;
-    if (hipMalloc(&p, c) != hipSuccess) return nullptr;
+    if (hipMalloc(&p, c) != hipSuccess) {
+      // cached blocks of other sizes may be what fills the device: release them, retry once
+      (void)hipGetLastError();
+      release(dev);
+      p = nullptr;
+      if (hipMalloc(&p, c) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+      }
+    }
+    std::lock_guard<std::mutex> lk(mu_);
+    owner_[p] = dev;
     return p;
   }
   void put(void* p, size_t bytes) {
@@ -100,13 +120,34 @@ class DevPool {
     const size_t c = size_class(bytes);
     {
       std::lock_guard<std::mutex> lk(mu_);
+      auto o = owner_.find(p);
+      const int dev = (o != owner_.end()) ? o->second : current_device();
       if (cached_ + c <= kCap) {
-        free_.emplace(c, p);
+        free_.emplace(std::make_pair(dev, c), p);
         cached_ += c;
         return;
       }
+      owner_.erase(p);
     }
     (void)hipFree(p);
+  }
+  // free every cached block of device dev
+  void release(int dev) {
+    std::vector<void*> victims;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      for (auto it = free_.begin(); it != free_.end();) {
+        if (it->first.first == dev) {
+          victims.push_back(it->second);
+          cached_ -= it->first.second;
+          owner_.erase(it->second);
+          it = free_.erase(it);
+        } else {
+          ++it;
+        }
+      }
+    }
+    for (void* v : victims) (void)hipFree(v);
   }
   size_t cached() {
     std::lock_guard<std::mutex> lk(mu_);
@@ -116,7 +157,8 @@ class DevPool {
  private:
   static constexpr size_t kCap = size_t(8) << 30;  // bytes kept cached (HBM is 288 GB)
   std::mutex mu_;
-  std::multimap<size_t, void*> free_;
+  std::multimap<std::pair<int, size_t>, void*> free_;  // (device, size class) -> block
+  std::map<void*, int> owner_;                         // block -> device it was allocated on
   size_t cached_ = 0;
 };
 
@@ -125,31 +167,39 @@ DevPool& dev_pool() {
   return *p;
 }
 
-// Non-blocking streams reused across calls (creating one costs ~10s of us).
+// Non-blocking streams reused across calls (creating one costs ~10s of us), one
+// free list per device: a stream is only handed to a caller whose current device
+// created it.
 class StreamPool {
  public:
   hipStream_t get() {
+    const int dev = current_device();
     {
       std::lock_guard<std::mutex> lk(mu_);
-      if (!free_.empty()) {
-        hipStream_t s = free_.back();
-        free_.pop_back();
+      auto& fl = free_[dev];
+      if (!fl.empty()) {
+        hipStream_t s = fl.back();
+        fl.pop_back();
         return s;
       }
     }
     hipStream_t s = nullptr;
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(mu_);
+    owner_[s] = dev;
     return s;
   }
   void put(hipStream_t s) {
     if (!s) return;
     std::lock_guard<std::mutex> lk(mu_);
-    free_.push_back(s);
+    auto o = owner_.find(s);
+    free_[o != owner_.end() ? o->second : current_device()].push_back(s);
   }
 
  private:
   std::mutex mu_;
-  std::vector<hipStream_t> free_;
+  std::map<int, std::vector<hipStream_t>> free_;
+  std::map<hipStream_t, int> owner_;
 };
 
 std::atomic<uint32_t> g_epoch{0};  // granule epoch of the next run (msa_plan_run)
@@ -270,10 +320,13 @@ struct msa_plan {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   uint32_t epoch = 0;
   unsigned long long* stamps = nullptr;  // diagnostic build
-  hipStream_t last_stream = nullptr;     // stream of the last run (msa_plan_destroy waits on it)
-  bool ran = false;
+  std::vector<hipStream_t> streams;      // every stream work of this plan was queued on
+                                         // (msa_plan_destroy waits on all of them)
   std::vector<std::pair<void*, size_t>> blocks;  // pooled device blocks owned by the plan
 
+  void note_stream(hipStream_t s) {
+    if (std::find(streams.begin(), streams.end(), s) == streams.end()) streams.push_back(s);
+  }
   // a pooled device block of `bytes`, owned by the plan
   template <class T>
   bool alloc(T** p, size_t bytes) {
@@ -360,10 +413,13 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   int tp = (kalg == MSA_ALG_SWL || kalg == MSA_ALG_SWL0 || kalg == MSA_ALG_SWA) ? (desc->track_end ? 1 : 0) : 0;
   if (tp) {
     // the first-maximum position packs with the value into one int (TRACKPOS 2) when every
-    // local score is below 2^16 (H <= match * min(m, n)) and a stripe has < 2^15 steps
+    // local score is below 2^16 and a stripe has < 2^15 steps.  A local score gains at
+    // most max(0, match, mismatch) per diagonal step (gaps only subtract), and a path
+    // has at most min(m, n) diagonal steps.
+    const int64_t smax = std::max({0, desc->match, desc->mismatch});
     bool pack = true;
     for (int64_t p = 0; p < desc->n_pairs && pack; ++p)
-      pack = (int64_t)std::max(0, desc->match) * std::min(desc->m[p], desc->n[p]) < 65536 && desc->n[p] + 512 < 32768;
+      pack = smax * std::min(desc->m[p], desc->n[p]) < 65536 && desc->n[p] + 512 < 32768;
     if (pack) tp = 2;
   }
   if (desc->single && desc->n_pairs != 1) { delete P; return MSA_ERR_ARG; }
@@ -419,8 +475,18 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
       // shifted recurrence G = H + g*(i+j): G must stay far from the -2^30 sentinel
       // and from int32 overflow; the profile byte holds score + 2g
       const int64_t g = kp.gap_open;
-      const int64_t top = g * (m + n + 2) + (int64_t)std::max(0, kp.match) * std::min(m, n);
-      if (g < 0 || top >= (int64_t(1) << 29) || kp.match + 2 * g > 127 || kp.mismatch + 2 * g < -128) {
+      const int64_t top = g * (m + n + 2) + (int64_t)std::max({0, kp.match, kp.mismatch}) * std::min(m, n);
+      const int64_t sm = kp.match + 2 * g, sx = kp.mismatch + 2 * g;  // profile bytes (int8)
+      if (g < 0 || top >= (int64_t(1) << 29) || sm > 127 || sm < -128 || sx > 127 || sx < -128) {
+        delete P;
+        return MSA_ERR_UNSUPPORTED;
+      }
+    }
+    if (kalg == MSA_ALG_SWA) {
+      // int8 profile bytes; H stays far from the -2^30 sentinel and from int32 overflow
+      const int64_t top = (int64_t)std::max({0, kp.match, kp.mismatch}) * std::min(m, n);
+      if (kp.match < -128 || kp.match > 127 || kp.mismatch < -128 || kp.mismatch > 127 || kp.gap_open < 0 ||
+          kp.gap_ext < 0 || top >= (int64_t(1) << 29)) {
         delete P;
         return MSA_ERR_UNSUPPORTED;
       }
@@ -581,8 +647,9 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
 
 void msa_plan_destroy(msa_plan* P) {
   if (!P) return;
-  // the plan's blocks go back to the pool: its last run must be complete
-  if (P->ran) (void)hipStreamSynchronize(P->last_stream);
+  // the plan's blocks go back to the pool: every run, traceback and score copy it
+  // queued (on whichever streams) must be complete
+  for (hipStream_t s : P->streams) (void)hipStreamSynchronize(s);
   for (auto& b : P->blocks) dev_pool().put(b.first, b.second);
   if (P->ev0) (void)hipEventDestroy(P->ev0);
   if (P->ev1) (void)hipEventDestroy(P->ev1);
@@ -612,8 +679,7 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
   if (P->d.cells != MSA_CELLS_NONE && !c0) return MSA_ERR_ARG;
   if (P->d.cells == MSA_CELLS_TAB && (!c1 || !c2)) return MSA_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
-  P->last_stream = st;
-  P->ran = true;
+  P->note_stream(st);
   KArgs a;
   std::memset(&a, 0, sizeof(a));
   a.kp = P->kp;
@@ -722,6 +788,7 @@ int msa_plan_clear_error(msa_plan* P, void* stream) {
 int msa_plan_scores(msa_plan* P, int32_t* dst, void* stream) {
   if (!P || !dst) return MSA_ERR_ARG;
   // the score field of every PairResult, device to device (no host sync)
+  P->note_stream((hipStream_t)stream);
   HIPCHK(hipMemcpy2DAsync(dst, sizeof(int32_t), P->d_res, sizeof(PairResult), sizeof(int32_t), (size_t)P->d.n_pairs,
                           hipMemcpyDeviceToDevice, (hipStream_t)stream));
   return MSA_OK;
@@ -739,10 +806,26 @@ int msa_plan_stripe_meta(msa_plan* P, int32_t* out, int64_t cap, void* stream) {
 int msa_plan_traceback(msa_plan* P, int64_t pair, const uint8_t* dDir, uint8_t* d_ops, int64_t ops_cap,
                        int64_t* d_info, void* stream) {
   if (!P || !dDir || !d_ops || !d_info || ops_cap < 0 || pair < 0 || pair >= P->d.n_pairs) return MSA_ERR_ARG;
-  if (P->kp.alg != MSA_ALG_SWA || P->d.cells != MSA_CELLS_DIR) return MSA_ERR_UNSUPPORTED;
+  // the walk starts at the fill's end cell: plans without track_end have none
+  if (P->kp.alg != MSA_ALG_SWA || P->d.cells != MSA_CELLS_DIR || !P->d.track_end) return MSA_ERR_UNSUPPORTED;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(sw_traceback_kernel, dim3(1), dim3(64), 0, st, dDir, P->d_pairs, P->d_meta,
-                     (const PairResult*)P->d_res, (int)pair, d_ops, (long long)ops_cap, (long long*)d_info);
+  P->note_stream(st);
+  hipLaunchKernelGGL(traceback_kernel<false>, dim3(1), dim3(64), 0, st, dDir, P->d_pairs, P->d_meta,
+                     (const PairResult*)P->d_res, (int)pair, 0, 0, d_ops, (long long)ops_cap, (long long*)d_info);
+  HIPCHK(hipGetLastError());
+  return MSA_OK;
+}
+
+int msa_plan_traceback_gotoh(msa_plan* P, int64_t pair, int end_type, const uint8_t* dDir, uint8_t* d_ops,
+                             int64_t ops_cap, int64_t* d_info, void* stream) {
+  if (!P || !dDir || !d_ops || !d_info || ops_cap < 0 || pair < 0 || pair >= P->d.n_pairs) return MSA_ERR_ARG;
+  if (end_type < -3 || end_type > 3 || end_type == 0) return MSA_ERR_ARG;
+  if (P->kp.alg != MSA_ALG_REF || P->d.cells != MSA_CELLS_DIR) return MSA_ERR_UNSUPPORTED;
+  hipStream_t st = (hipStream_t)stream;
+  P->note_stream(st);
+  hipLaunchKernelGGL(traceback_kernel<true>, dim3(1), dim3(64), 0, st, dDir, P->d_pairs, P->d_meta,
+                     (const PairResult*)P->d_res, (int)pair, end_type, (int)P->kp.h, d_ops, (long long)ops_cap,
+                     (long long*)d_info);
   HIPCHK(hipGetLastError());
   return MSA_OK;
 }

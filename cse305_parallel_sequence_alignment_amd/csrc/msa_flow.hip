@@ -237,10 +237,15 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
   const int grp = (int)(blockIdx.x & 7), chunk = kp.sched_cap;
 
   if constexpr (SAVE) {
-    if ((int)blockIdx.x >= a.nflow) {
-      // pass-2 workgroup: every wave takes blocks on its own, in expected readiness
-      // order.  Workgroups are dispatched in index order, so the pass-1 workgroups
-      // (the lowest indices) are resident before any of these waits on them.
+    // Role by arrival, not by blockIdx: the first nflow workgroups to START run pass 1,
+    // the later ones pass-2 blocks.  A pass-2 block waits only on pass-1 outputs, and
+    // every pass-1 role is held by a workgroup that is already running (and stays
+    // resident until every item is claimed), so progress does not depend on the order
+    // in which the hardware dispatches workgroups, or on CUs held by other kernels.
+    if (threadIdx.x == 0) smem[1] = atomicAdd(a.ticket + 13, 1);
+    __syncthreads();
+    if (uni(smem[1]) >= a.nflow) {
+      // pass-2 workgroup: every wave takes blocks on its own, in expected readiness order
       for (;;) {
         // (a separate, non-inlined block function keeps this loop's control flow
         // uniform: inlined, the structurizer re-entered it without the ticket)

@@ -1,12 +1,23 @@
-// msa_traceback.hip -- on-device Smith-Waterman traceback (config C5).
+// msa_traceback.hip -- on-device traceback walks over direction bytes.
 //
-// The fill (stripe_kernel, MSA_ALG_SWA, MSA_OUT_DIR) leaves one direction byte
-// per cell in the skewed stripe layout: cell (64s + r + 1, cs_s + t - r) at
+//  * SW affine (config C5): the fill (stripe_kernel, MSA_ALG_SWA, MSA_OUT_DIR)
+//    leaves one byte per cell -- bits 0-1: where H came from (0 = local start,
+//    1 = diagonal, 2 = E / horizontal gap, 3 = F / vertical gap); bit 2: E here
+//    opened from H(i, j-1); bit 3: F here opened from H(i-1, j).  The walk is the
+//    tie order of oracle orc_sw (first maximum), from the pair's end cell.
+//  * Reference Gotoh (MSA_ALG_REF, MSA_OUT_DIR: main_alignment_function /
+//    Subproblem::find_alignment, subproblem_alignment.cpp:105-172): bits 0-1 =
+//    T1's predecessor table, 2-3 = T2's, 4-5 = T3's (1..3, the first table in
+//    the reference's order T1, T2, T3 whose value reproduces the cell by exact
+//    equality).  The walk starts at (m, n) in the end node's table (the
+//    reference's end-type rule, :112-146, from the fill's final state) and stops
+//    when i == 0 or j == 0 (:147).  One op per step = the table the step leaves
+//    from ('M' T1 / diagonal, 'D' T2 / consumes B, 'I' T3 / consumes A); the host
+//    turns them into the reference's align list (node coordinates, quirks Q1/Q2).
+//
+// Both layouts are the skewed stripe layout: cell (64s + r + 1, cs_s + t - r) at
 // byte (s*pmax + t/16)*1024 + r*16 + t%16 of the pair's block -- a 16-step x
-// 64-row block is 1 KiB, one 16-byte row segment per lane.  Bits 0-1: where H
-// came from (0 = local start, 1 = diagonal, 2 = E / horizontal gap, 3 = F /
-// vertical gap); bit 2: E here opened from H(i, j-1); bit 3: F here opened from
-// H(i-1, j).  The walk is the tie order of oracle orc_sw (first maximum).
+// 64-row block is 1 KiB, one 16-byte row segment per lane.
 //
 // One wave walks the path from the pair's end cell (read from the reduction's
 // PairResult on the same stream, no host round trip).  Its state is uniform
@@ -62,20 +73,43 @@ constexpr unsigned long long TB_FH = (27ull << 4) | (9ull << 16) | ((9ull << 4) 
 
 __device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" : : : "memory"); }
 
-__global__ __launch_bounds__(64) void sw_traceback_kernel(const uint8_t* __restrict__ dir,
-                                                          const msa_pair_desc* __restrict__ pairs,
-                                                          const msa_stripe_meta* __restrict__ meta,
-                                                          const PairResult* __restrict__ res, int pair,
-                                                          uint8_t* __restrict__ ops, long long cap,
-                                                          long long* __restrict__ info) {
+// find_alignment's end node table (subproblem_alignment.cpp:112-146) from the final
+// state fin = (T1, T2, T3)(m, n), MSA_NEG = -inf: end_type > 0 names it; otherwise
+// the first of T1, T2 + h', T3 + h' that is >= the others (h' = h for the table
+// end_type <= -2 names).  Returns 0, 1, 2 for T1, T2, T3.
+__device__ __forceinline__ int ref_end_state(const int32_t (&fin)[3], int end_type, int h) {
+  if (end_type > 0) return end_type - 1;
+  const long long NI = -(1ll << 62);  // -inf: absorbs + h
+  auto v = [&](int k) {
+    const long long x = fin[k];
+    return x == (long long)MSA_NEG ? NI : x + ((k + 1 == -end_type && end_type <= -2) ? h : 0);
+  };
+  const long long t1 = v(0), t2 = v(1), t3 = v(2);
+  if (t1 >= t2 && t1 >= t3) return 0;
+  if (t2 >= t1 && t2 >= t3) return 1;
+  return 2;
+}
+
+// REF = false: Smith-Waterman affine walk; true: the reference's Gotoh walk (end_type,
+// h: find_alignment's end rule).
+template <bool REF>
+__global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict__ dir,
+                                                       const msa_pair_desc* __restrict__ pairs,
+                                                       const msa_stripe_meta* __restrict__ meta,
+                                                       const PairResult* __restrict__ res, int pair, int end_type,
+                                                       int hpen, uint8_t* __restrict__ ops, long long cap,
+                                                       long long* __restrict__ info) {
   const int lane = threadIdx.x;
   const msa_pair_desc pd = pairs[pair];
   const PairResult r0 = res[pair];
   const uint8_t* base = dir + pd.out_off + lane * 16;
   const int pmax = pd.pmax;
-  int i = (int)r0.end_i, j = (int)r0.end_j;  // plans hold m, n < 2^26
+  // plans hold m, n < 2^26
+  int i = REF ? pd.m : (int)r0.end_i, j = REF ? pd.n : (int)r0.end_j;
   int nops = 0;
-  int st = 0;  // 0: in H, 1: in E (horizontal gap), 2: in F (vertical gap)
+  // SW: 0 in H, 1 in E (horizontal gap), 2 in F (vertical gap); REF: 0, 1, 2 = T1, T2, T3
+  int st = 0;
+  if constexpr (REF) st = ref_end_state(r0.fin, end_type, hpen);
   int status = 0;
   __shared__ __attribute__((aligned(16))) uint8_t stage[2][4096];  // current group / the one being fetched
   typedef __attribute__((address_space(3))) uint8_t lds_u8;
@@ -147,7 +181,7 @@ __global__ __launch_bounds__(64) void sw_traceback_kernel(const uint8_t* __restr
     vm_wait_all();
     t_wait += (long long)__builtin_amdgcn_s_memtime() - a;
   };
-  if (r0.score > 0) {
+  if (REF || r0.score > 0) {
     bool stopped = false;
     // outer iteration: make the group under (i, j) current, keep the next one in flight,
     // then run the steps that provably stay inside the group without any further checks
@@ -231,10 +265,18 @@ __global__ __launch_bounds__(64) void sw_traceback_kernel(const uint8_t* __restr
         unsigned raw = grp[ga];
         asm("" : "+v"(raw));  // keep the read unconditional
         const unsigned dv = in_grp ? raw : 0u;
-        const unsigned fH = (unsigned)(TB_FH >> (16 * (dv & 3u))) & 0x1ffu;
-        const unsigned fE = 1u | ((dv & 4u) ? 0u : (9u << 4));
-        const unsigned fF = 8u | ((dv & 8u) ? 0u : (18u << 4));
-        const int wt = (int)(fH | (fE << 9) | (fF << 18));
+        int wt;
+        if constexpr (REF) {
+          // table s (T1, T2, T3) leaves by its fixed move (diagonal 9, left 1, up 8) into the
+          // table bits 2s..2s+1 name; 0 there (no predecessor) stops the walk with an error
+          auto fld = [](unsigned step, unsigned nt) { return step | ((nt ? 9u * (nt - 1u) : 27u) << 4); };
+          wt = (int)(fld(9u, dv & 3u) | (fld(1u, (dv >> 2) & 3u) << 9) | (fld(8u, (dv >> 4) & 3u) << 18));
+        } else {
+          const unsigned fH = (unsigned)(TB_FH >> (16 * (dv & 3u))) & 0x1ffu;
+          const unsigned fE = 1u | ((dv & 4u) ? 0u : (9u << 4));
+          const unsigned fF = 8u | ((dv & 8u) ? 0u : (18u << 4));
+          wt = (int)(fH | (fE << 9) | (fF << 18));
+        }
         int idx = 0, k = 0;
         unsigned wcode = 0;
         if (kmax == 7) {
@@ -277,14 +319,19 @@ __global__ __launch_bounds__(64) void sw_traceback_kernel(const uint8_t* __restr
       st = stop ? 3 : sh / 9;
       i -= r_in - r;                  // rows consumed
       j -= (t_in - t) - (r_in - r);   // columns consumed
-      if (st == 3) {  // local start (H came from 0): the walk ends at this cell
+      if constexpr (REF) {
+        // a cell without a predecessor table (cannot happen for a complete fill)
+        if (st == 3) { status = -9; stopped = true; }  // MSA_ERR_NOMATCH
+        // find_alignment stops at the matrix border (:147); the budget (<= min(i, j)) makes
+        // a window end exactly there
+      } else if (st == 3) {  // local start (H came from 0): the walk ends at this cell
         st = 0;
         stopped = true;
       }
     }
   }
   decode();  // the words still in the ring
-  if (nops > cap) status = -8;  // MSA_ERR_CAPACITY
+  if (nops > cap && status == 0) status = -8;  // MSA_ERR_CAPACITY
   if (pend) vm_wait_all();  // no load left in flight when the wave ends
   if (lane == 0) {
     info[0] = nops;

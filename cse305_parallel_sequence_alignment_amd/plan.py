@@ -173,11 +173,41 @@ class Plan:
         ops = torch.empty(self.ms[pair] + self.ns[pair] + 2, dtype=torch.uint8, device=dev)
         info = torch.zeros(8, dtype=torch.int64, device=dev)
         self.traceback_async(dDir, ops, info, pair, stream)
+        if stream is not None:
+            # .cpu() below orders only against torch's current stream: wait for the walk's own
+            (torch.cuda.ExternalStream(stream) if isinstance(stream, int) else stream).synchronize()
         inf = info.cpu().tolist()
         LB.check(int(inf[3]), "msa_plan_traceback")
         o = bytes(ops[:inf[0]].cpu().numpy().tobytes())
         return dict(ops=o, beg=(int(inf[1]), int(inf[2])), cigar=cigar_of(o),
                     stats=dict(switches=int(inf[4]), on_demand=int(inf[5]), ticks=int(inf[6]), wait_ticks=int(inf[7])))
+
+    def traceback_gotoh_async(self, dDir, d_ops, d_info, end_type=-1, pair=0, stream=None) -> None:
+        """Device find_alignment walk (msa_plan_traceback_gotoh) of a REF_GOTOH DIR plan, stream-ordered after
+        run(): d_ops (uint8, >= m+n) receives one op per step end -> start ('M' T1, 'D' T2, 'I' T3), d_info
+        (int64[8]) {n_ops, i+1, j+1, status, ...} with (i, j) the border cell the walk stopped at."""
+        import torch
+
+        if not (dDir.is_cuda and dDir.dtype == torch.uint8 and dDir.numel() >= self.cells_elems):
+            raise ValueError("dDir must be the uint8 CUDA tensor the plan's run() wrote")
+        if not (d_ops.is_cuda and d_ops.dtype == torch.uint8 and d_ops.is_contiguous()):
+            raise ValueError("d_ops must be a contiguous uint8 CUDA tensor")
+        if not (d_info.is_cuda and d_info.dtype == torch.int64 and d_info.numel() >= 8):
+            raise ValueError("d_info must be an int64 CUDA tensor of >= 8 elements")
+        LB.check(LB.lib().msa_plan_traceback_gotoh(self._h, pair, end_type, _ptr(dDir), _ptr(d_ops), d_ops.numel(),
+                                                   _ptr(d_info), _stream_ptr(stream)), "msa_plan_traceback_gotoh")
+
+    def traceback_gotoh(self, dDir, end_type=-1, pair=0):
+        """Device find_alignment walk, fetched: dict(ops=bytes end -> start, stop=(i, j))."""
+        import torch
+
+        dev = dDir.device
+        ops = torch.empty(self.ms[pair] + self.ns[pair] + 2, dtype=torch.uint8, device=dev)
+        info = torch.zeros(8, dtype=torch.int64, device=dev)
+        self.traceback_gotoh_async(dDir, ops, info, end_type, pair)
+        inf = info.cpu().tolist()
+        LB.check(int(inf[3]), "msa_plan_traceback_gotoh")
+        return dict(ops=bytes(ops[:inf[0]].cpu().numpy().tobytes()), stop=(int(inf[1]) - 1, int(inf[2]) - 1))
 
     def set_timing(self, on: bool) -> None:
         """Record HIP events around the DP kernel in run() (default on; kernel_ms() needs it)."""

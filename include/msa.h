@@ -252,6 +252,20 @@ int msa_plan_pair_layout(const msa_plan* plan, int64_t pair, int64_t* out4);
  * no host sync; tie order of the oracle's orc_sw. */
 int msa_plan_traceback(msa_plan* plan, int64_t pair, const uint8_t* dDir, uint8_t* d_ops, int64_t ops_cap,
                        int64_t* d_info, void* stream);
+/* Subproblem::find_alignment ON THE DEVICE (replaces the host walk over the
+ * reference's T1/T2/T3 tables, subproblem_alignment.cpp:105-172) for an
+ * MSA_REF_GOTOH plan with MSA_CELLS_DIR, after msa_plan_run on the same stream:
+ * one wave starts at (m, n) in the table the reference's end rule picks for
+ * end_type (:112-146, from the run's final state; end_type in {-3..-1, 1..3})
+ * and walks the direction bytes until i == 0 or j == 0 (:147).  d_ops receives
+ * one op per step, end -> start: the table the step leaves ('M' T1 / diagonal,
+ * 'D' T2 / consumes B, 'I' T3 / consumes A; at most ops_cap, m+n suffices);
+ * d_info[8] as msa_plan_traceback, with {n_ops, i+1, j+1, status} where (i, j)
+ * is the border cell the walk stopped at and status 0, MSA_ERR_CAPACITY or
+ * MSA_ERR_NOMATCH.  The reference's align nodes (coordinates, quirks Q1/Q2)
+ * follow from the ops on the host in O(m+n) (msa_main_alignment does this). */
+int msa_plan_traceback_gotoh(msa_plan* plan, int64_t pair, int end_type, const uint8_t* dDir, uint8_t* d_ops,
+                             int64_t ops_cap, int64_t* d_info, void* stream);
 /* Order-independent digest of pair `pair`'s H cells (oracle orc_checksum_h). */
 int msa_plan_checksum(msa_plan* plan, const int32_t* dH, int64_t pair, uint64_t* digest, void* stream);
 /* Device time (ms) of the last msa_plan_run's stripe kernel, from HIP events

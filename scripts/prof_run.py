@@ -26,6 +26,11 @@ elif wl == "c5":
     A, B = data.c5_pair(0, False)  # the bench's C5 pair
     pl = Plan(LB.SW_AFFINE, LB.CELLS_DIR, [20000], [20000], [0], [0], match=1, mismatch=0, gap_open=3,
               gap_extend=1, track_end=True)
+elif wl in ("ref", "ref20"):
+    L = 10000 if wl == "ref" else 20000
+    A, B = seqs[0][:L], seqs[1][:L]  # the bench's ref pair (main_alignment_function's path)
+    pl = Plan(LB.REF_GOTOH, LB.CELLS_DIR, [L], [L], [0], [0], match=1, mismatch=0, gap_open=3, gap_extend=1,
+              start_type=-1)
 elif wl == "c3":
     from cse305_parallel_sequence_alignment_amd import data
 
@@ -44,12 +49,15 @@ if pl.cells != LB.CELLS_NONE:
     out = torch.empty(pl.cells_elems, dtype=torch.uint8 if pl.cells == LB.CELLS_DIR else torch.int32, device="cuda")
 dA, dB = enc(A), enc(B)
 tb = None
-if wl == "c5":  # the bench's C5 step: fill, then the traceback on the device
+if wl in ("c5", "ref", "ref20"):  # the bench's step: fill, then the traceback walk on the device
     tb = (torch.empty(len(A) + len(B) + 2, dtype=torch.uint8, device="cuda"),
           torch.zeros(8, dtype=torch.int64, device="cuda"))
 for _ in range(reps):
     pl.run(dA, dB, out)
     if tb is not None:
-        pl.traceback_async(out, *tb)
+        if wl == "c5":
+            pl.traceback_async(out, *tb)
+        else:
+            pl.traceback_gotoh_async(out, *tb, -1)
 torch.cuda.synchronize()
 print("score", pl.results()[0]["score"], "kernel_ms", pl.kernel_ms())

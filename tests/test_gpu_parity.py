@@ -566,3 +566,122 @@ def test_sticky_error_word(dev, LB):
     assert pl.error() == 0
     pl.clear_error()
     assert pl.error() == 0
+
+
+def _mutated(rng, m, n):
+    """B = a mutated copy of A (substitutions + short indels), trimmed / extended to n."""
+    A = rs(rng, m)
+    b = bytearray(A[:n] if n <= m else A + rs(rng, n - m))
+    for k in rng.choice(len(b), size=max(1, len(b) // 15), replace=False):
+        b[k] = ACGT[rng.integers(4)]
+    return A, bytes(b[:n]) + rs(rng, max(0, n - len(b)))
+
+
+@pytest.mark.parametrize("gh", [(1, 2), (2, 1), (1, 0), (3, 5)])
+@pytest.mark.parametrize("st,en", [(-1, -1), (-2, -3), (-3, -2), (1, 2), (3, 1), (2, -1)])
+def test_gotoh_device_walk(oracle, dev, LB, gh, st, en):
+    """find_alignment ON THE DEVICE (msa_plan_traceback_gotoh) over a REF_GOTOH DIR fill: the walk's ops are
+    the tables of the oracle's node list (end node first), every start / end type, several (g, h), shapes
+    from one row-block to many stripes and 16-step blocks."""
+    import torch
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+
+    g, h = gh
+    rng = np.random.default_rng(100 + 7 * g + h + 13 * st + en)
+    for (m, n) in [(1, 1), (1, 40), (5, 300), (64, 64), (65, 66), (129, 700), (700, 701), (1000, 1300)]:
+        A, B = _mutated(rng, m, n) if m > 100 else (rs(rng, m), rs(rng, n))
+        pl = Plan(LB.REF_GOTOH, LB.CELLS_DIR, [m], [n], [0], [0], match=1, mismatch=0, gap_open=g + h,
+                  gap_extend=g, start_type=st)
+        D = torch.empty(pl.cells_elems, dtype=torch.uint8, device=dev)
+        pl.run(_dev(A, dev), _dev(B, dev), D)
+        tb = pl.traceback_gotoh(D, end_type=en)
+        o = oracle.subproblem_align(A, B, st, en, float(g), float(h))
+        ts = [t for (_, _, t) in o["nodes"]]
+        # op k = the table step k leaves = node t's end -> start; the end node's table first
+        want = "".join("MDI"[t - 1] for t in reversed(ts)) if ts else "MDI"[o["end"][2] - 1]
+        assert tb["ops"].decode() == want, (m, n, st, en)
+        assert tb["ops"][:1].decode() == "MDI"[o["end"][2] - 1]
+        assert min(tb["stop"]) == 0 and max(tb["stop"]) >= 0, tb["stop"]
+
+
+def test_gotoh_walk_rejects_wrong_plans(dev, LB):
+    """msa_plan_traceback_gotoh needs a REF_GOTOH DIR plan and a valid end type; msa_plan_traceback needs an
+    SW-affine DIR plan created with track_end (its walk starts at the fill's end cell)."""
+    import torch
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+
+    rng = np.random.default_rng(5)
+    A, B = rs(rng, 50), rs(rng, 60)
+    ref = Plan(LB.REF_GOTOH, LB.CELLS_DIR, [50], [60], [0], [0], gap_open=3, gap_extend=1)
+    D = torch.empty(ref.cells_elems, dtype=torch.uint8, device=dev)
+    ref.run(_dev(A, dev), _dev(B, dev), D)
+    with pytest.raises(LB.MsaError) as e:
+        ref.traceback_gotoh(D, end_type=0)
+    assert e.value.status == -1
+    with pytest.raises(LB.MsaError) as e:
+        ref.traceback(D)  # the SW walk on a Gotoh plan
+    assert e.value.status == -5
+    sw = Plan(LB.SW_AFFINE, LB.CELLS_DIR, [50], [60], [0], [0], match=1, mismatch=0, gap_open=3, gap_extend=1,
+              track_end=False)
+    D2 = torch.empty(sw.cells_elems, dtype=torch.uint8, device=dev)
+    sw.run(_dev(A, dev), _dev(B, dev), D2)
+    with pytest.raises(LB.MsaError) as e:
+        sw.traceback(D2)  # no end cell without track_end
+    assert e.value.status == -5
+    with pytest.raises(LB.MsaError) as e:
+        sw.traceback_gotoh(D2)
+    assert e.value.status == -5
+
+
+@pytest.mark.parametrize("alg", ["linear", "affine"])
+def test_packed_end_tracking_mismatch_above_match(oracle, dev, LB, alg):
+    """The packed first-maximum key (value << 15) is chosen from max(0, match, mismatch) * min(m, n) < 2^16:
+    with mismatch > match the local scores grow by the mismatch, and the plan must still report the
+    oracle's score and end cell (it picks the packed or the compare-select tracking accordingly)."""
+    import torch
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+
+    rng = np.random.default_rng(21)
+    for (m, n, ma, mi) in [(300, 280, 1, 3), (3000, 2900, 1, 40), (700, 650, 2, 5)]:
+        A, B = rs(rng, m), rs(rng, n)
+        if alg == "linear":
+            pl = Plan(LB.SW_LINEAR, LB.CELLS_NONE, [m], [n], [0], [0], match=ma, mismatch=mi, gap_open=1,
+                      gap_extend=1, track_end=True)
+            pl.run(_dev(A, dev), _dev(B, dev))
+            o = oracle.sw(A, B, ma, mi, 1, 1)
+        else:
+            pl = Plan(LB.SW_AFFINE, LB.CELLS_NONE, [m], [n], [0], [0], match=ma, mismatch=mi, gap_open=3,
+                      gap_extend=1, track_end=True)
+            pl.run(_dev(A, dev), _dev(B, dev))
+            o = oracle.sw(A, B, ma, mi, 3, 1)
+        r = pl.results()[0]
+        assert (r["score"], tuple(r["end"])) == (o["score"], tuple(o["end"])), (m, n, ma, mi)
+
+
+def test_c2_plan_under_contention(oracle, dev, LB):
+    """The two-pass C2 flow kernel (pass-1 / pass-2 roles by arrival ticket) while long GEMMs occupy CUs on
+    another stream: the sticky error word stays 0 and the full-H checksum equals the oracle's."""
+    import torch
+    from cse305_parallel_sequence_alignment_amd import data
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+
+    A, B = data.c2_pair(0)
+    A, B = A[:6000], B[:6000]
+    pl = Plan(LB.SW_LINEAR, LB.CELLS_H, [len(A)], [len(B)], [0], [0], match=1, mismatch=0, gap_open=1,
+              gap_extend=1)
+    H = torch.empty(pl.cells_elems, dtype=torch.int32, device=dev)
+    dA, dB = _dev(A, dev), _dev(B, dev)
+    busy = torch.cuda.Stream(device=dev)
+    mine = torch.cuda.Stream(device=dev)
+    x = torch.randn(4096, 4096, device=dev, dtype=torch.bfloat16)
+    torch.cuda.synchronize()
+    for _ in range(3):
+        with torch.cuda.stream(busy):
+            for _ in range(30):
+                x = torch.tanh(x @ x * 1e-3)
+        pl.run(dA, dB, H, stream=mine)
+    torch.cuda.synchronize()
+    assert pl.error() == 0
+    o = oracle.sw(A, B, 1, 0, 1, 1, want_h=True)
+    assert pl.results()[0]["score"] == o["score"]
+    assert pl.checksum(H) == oracle.checksum_h(o["H"])
