@@ -97,6 +97,7 @@ def lib() -> C.CDLL:
     L.msa_plan_run.argtypes = [P, P, P, P, P, P, P]
     L.msa_plan_results.argtypes = [P, P, P]
     L.msa_plan_error.argtypes = [P, C.POINTER(C.c_int), P]
+    L.msa_plan_run_info.argtypes = [P, P, P]
     L.msa_plan_clear_error.argtypes = [P, P]
     L.msa_plan_scores.argtypes = [P, P, P]
     L.msa_plan_stripe_meta.argtypes = [P, P, i64, P]
@@ -131,7 +132,7 @@ EXPORTED = [
     "msa_non_parallel_tables", "msa_optimal_alignment", "msa_main_alignment_partitioned",
     "msa_subproblem_f64", "msa_subproblem_row",
     "msa_partial_partition", "msa_partial_tables", "msa_plan_create", "msa_plan_destroy", "msa_plan_cells_size",
-    "msa_plan_run", "msa_plan_results", "msa_plan_error", "msa_plan_clear_error", "msa_plan_scores",
+    "msa_plan_run", "msa_plan_results", "msa_plan_error", "msa_plan_run_info", "msa_plan_clear_error", "msa_plan_scores",
     "msa_plan_stripe_meta", "msa_plan_stripes", "msa_plan_pair_layout",
     "msa_plan_checksum", "msa_plan_traceback", "msa_plan_traceback_gotoh",
     "msa_plan_last_kernel_ms", "msa_plan_set_timing", "msa_encode_pair", "msa_sw_align",

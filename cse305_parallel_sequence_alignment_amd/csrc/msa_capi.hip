@@ -323,6 +323,20 @@ struct msa_plan {
   std::vector<hipStream_t> streams;      // every stream work of this plan was queued on
                                          // (msa_plan_destroy waits on all of them)
   std::vector<std::pair<void*, size_t>> blocks;  // pooled device blocks owned by the plan
+  // chunked banded single pair (kp.single == 2, rank convergence): the main launch runs the
+  // chunks; the exact single-mode launch (fb_*) is queued behind it and exits at once
+  // unless a chunk failed to converge
+  bool chunked = false;
+  int n_chunks = 0;
+  msa_kparams fb_kp;
+  kfn_t fb_fn = nullptr;
+  int fb_grid = 1, fb_threads = 64;
+  size_t fb_lds = 0;
+  int* d_ck = nullptr;  // [chunk][2][2][ckw] band states (msa_kernels.hip)
+  int ckw = 0;
+  int* d_dk = nullptr;    // per-chunk constant d_k
+  int* d_okk = nullptr;   // per-chunk converged flag
+  int* d_skip = nullptr;  // 1: every chunk converged (the exact launch exits)
 
   void note_stream(hipStream_t s) {
     if (std::find(streams.begin(), streams.end(), s) == streams.end()) streams.push_back(s);
@@ -589,6 +603,50 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     P->nflow = P->grid;
     if (P->flow2) P->grid = std::max(P->grid + 8, 8 * per_xcd);
   }
+  // Banded single pair (C3-type): the band has only ~9 stripes in flight, so the exact
+  // launch is one long chain of ~S x 8 phases.  Chunked mode runs it as n_chunks
+  // independent chains of chunk_c (+ warm-up) stripes at once (rank convergence,
+  // msa_kernels.hip header), with the exact launch kept behind it as the fallback.
+  constexpr int kWarm = 24;  // warm-up stripes (1,536 rows): C3's pair converges within ~900
+  if (single && kalg == MSA_ALG_NWA && band >= 0 && (out_mode == MSA_OUT_H || out_mode == MSA_OUT_NONE)) {
+    const int S = (int)((desc->m[0] + 63) / 64);
+    const int cc = std::max(kWarm, (S + prop.multiProcessorCount - 1) / prop.multiProcessorCount);
+    const int nch = (S + cc - 1) / cc;
+    kfn_t cfn = pick_kernel(kalg, out_mode, 0, false);
+    if (nch >= 4 && cfn) {
+      P->chunked = true;
+      P->n_chunks = nch;
+      P->fb_kp = kp;
+      P->fb_fn = P->fn;
+      P->fb_grid = P->grid;
+      P->fb_threads = P->threads;
+      P->fb_lds = P->lds_bytes;
+      kp.single = 2;
+      kp.chunk_c = cc;
+      kp.chunk_warm = kWarm;
+      kp.n_items = nch;
+      kp.sched_cap = cc + kWarm;
+      kp.lds_row_words = ((max_P * MSA_K + MSA_ROWOFF + 32) + 15) & ~15;
+      P->fn = cfn;
+      P->W = MSA_WAVES_BATCH;
+      P->threads = (MSA_WAVES_BATCH + 1) * 64;
+      P->lds_bytes = (16 + (size_t)kp.sched_cap * 8 + (size_t)(2 * MSA_WAVES_BATCH + 1) * P->nc * MSA_RING +
+                      (size_t)P->nc * kp.lds_row_words) * 4;
+      if (P->lds_bytes > 160 * 1024 ||
+          hipFuncSetAttribute((const void*)P->fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P->lds_bytes) !=
+              hipSuccess) {
+        delete P;
+        return MSA_ERR_UNSUPPORTED;
+      }
+      int occ2 = 1;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ2, (const void*)P->fn, P->threads, P->lds_bytes) !=
+              hipSuccess || occ2 < 1)
+        occ2 = 1;
+      // every chunk at once (one workgroup each); more chunks than slots just queue
+      P->grid = std::max(1, std::min(nch, prop.multiProcessorCount * std::min(occ2, 2)));
+      P->ckw = (2 * band + 1 + 3) & ~3;
+    }
+  }
   // device buffers
   auto fail = [&](void) { msa_plan_destroy(P); return MSA_ERR_HIP; };
   if (!P->alloc(&P->d_pairs, sizeof(msa_pair_desc) * P->pairs.size())) return fail();
@@ -608,9 +666,10 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     return fail();
   if (!P->alloc(&P->d_res, sizeof(PairResult) * desc->n_pairs)) return fail();
   if (!P->alloc(&P->d_sum, 64)) return fail();
-  if (single && kp.n_items > 1) {
+  const int single_items = P->chunked ? P->fb_kp.n_items : kp.n_items;  // single-mode launch's items
+  if (single && single_items > 1) {
     P->gbuf_stride = (int)(((desc->n[0] + 2 * MSA_GOFF + 16) + 15) & ~15);
-    const size_t gb = (size_t)(kp.n_items - 1) * P->nc * P->gbuf_stride * sizeof(unsigned long long);
+    const size_t gb = (size_t)(single_items - 1) * P->nc * P->gbuf_stride * sizeof(unsigned long long);
     if (!P->alloc(&P->d_gbuf, gb)) return fail();
     if (hipMemset(P->d_gbuf, 0, gb) != hipSuccess) return fail();
   }
@@ -635,6 +694,14 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     if (!P->alloc(&P->d_blk, sizeof(int4) * (size_t)P->nblk)) return fail();
     if (!P->alloc(&P->d_order, sizeof(int) * (size_t)P->nblk)) return fail();
     if (hipMemcpy(P->d_order, order.data(), sizeof(int) * (size_t)P->nblk, hipMemcpyHostToDevice) != hipSuccess)
+      return fail();
+  }
+  if (P->chunked) {
+    const size_t ckb = sizeof(int) * (size_t)P->n_chunks * 4 * P->ckw;
+    // entries a chunk never writes (outside the band row / matrix) read as -inf
+    if (!P->alloc(&P->d_ck, ckb) || hipMemset(P->d_ck, 0xC0, ckb) != hipSuccess) return fail();
+    if (!P->alloc(&P->d_dk, sizeof(int) * P->n_chunks) || !P->alloc(&P->d_okk, sizeof(int) * P->n_chunks) ||
+        !P->alloc(&P->d_skip, 64))
       return fail();
   }
   if (hipEventCreate(&P->ev0) != hipSuccess || hipEventCreate(&P->ev1) != hipSuccess) return fail();
@@ -721,8 +788,31 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
   const bool ev = P->timing;  // timing events are instrumentation: msa_plan_set_timing
   if (ev) HIPCHK(hipEventRecord(P->ev0, st));
   P->timed = ev;
+  if (P->chunked) {
+    a.ck = P->d_ck;
+    a.ckw = P->ckw;
+  }
   hipLaunchKernelGGL(P->fn, dim3(P->grid), dim3(P->threads), P->lds_bytes, st, a);
   HIPCHK(hipGetLastError());
+  if (P->chunked) {
+    // verify every chunk's constant, add the prefix of the constants to its cells; then the
+    // exact single-mode launch, which returns at once when *skip == 1
+    hipLaunchKernelGGL(chunk_check_kernel, dim3(P->n_chunks), dim3(256), 0, st, (const int*)P->d_ck, P->ckw, P->d_dk,
+                       P->d_okk);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(chunk_add_kernel, dim3(32, P->n_chunks), dim3(256), 0, st,
+                       P->d.cells == MSA_CELLS_H ? a.outH : (int32_t*)nullptr, (const msa_pair_desc*)P->d_pairs,
+                       P->d_meta, (const int*)P->d_dk, (const int*)P->d_okk, P->n_chunks, P->kp.chunk_c, P->d_skip,
+                       P->d_ticket);
+    HIPCHK(hipGetLastError());
+    KArgs b = a;
+    b.kp = P->fb_kp;
+    b.kp.epoch = ep;
+    b.ck = nullptr;
+    b.skip = P->d_skip;
+    hipLaunchKernelGGL(P->fb_fn, dim3(P->fb_grid), dim3(P->fb_threads), P->fb_lds, st, b);
+    HIPCHK(hipGetLastError());
+  }
   if (ev) HIPCHK(hipEventRecord(P->ev1, st));
   if (P->flow2) {
     hipLaunchKernelGGL(reduce_blocks_kernel, dim3(1), dim3(1024), 0, st, (const int4*)P->d_blk, P->nblk, P->d_res);
@@ -767,6 +857,22 @@ int msa_plan_results(msa_plan* P, msa_pair_result* out, void* stream) {
     std::fprintf(stderr, "msa: a kernel wait hit its spin limit (site %d) in a run since the plan was created "
                  "or last cleared\n", err);
     return MSA_ERR_TIMEOUT;
+  }
+  return MSA_OK;
+}
+
+int msa_plan_run_info(msa_plan* P, int32_t* out4, void* stream) {
+  if (!P || !out4) return MSA_ERR_ARG;
+  out4[0] = P->chunked ? 2 : (P->flow ? 1 : 0);
+  out4[1] = P->n_chunks;
+  out4[2] = -1;
+  out4[3] = P->chunked ? P->kp.chunk_warm : 0;
+  if (P->chunked) {
+    int v = 0;
+    hipStream_t st = (hipStream_t)stream;
+    HIPCHK(hipMemcpyAsync(&v, P->d_skip, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    out4[2] = v;
   }
   return MSA_OK;
 }

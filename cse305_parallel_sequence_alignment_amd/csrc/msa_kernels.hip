@@ -29,11 +29,23 @@
 //    (1 KiB per wave instruction).  Layout: element (s, t, r) of pair block
 //    = ((s * pmax*4 + t/4) * 64 + r) * 4 + t%4   <->   cell (64s+r+1, cs_s+t-r).
 //
-// Two launch modes share the kernel:
+// Three launch modes share the kernel:
 //  * single: one pair, items = groups of W stripes, tickets in order
 //    (a workgroup only ever waits on an earlier ticket -> no deadlock).
 //  * batch: items = whole pairs; wave w runs stripes w, w+W, ...; the
 //    wave W-1 -> wave 0 wrap link goes through a full LDS row buffer.
+//  * chunked (banded single pair, rank convergence): items = chunks of
+//    chunk_c consecutive stripes, each run batch-style by one workgroup, all
+//    at once.  Chunk k starts chunk_warm stripes before its first stripe from a
+//    GUESSED row (a tent shaped like the row-0 border) instead of waiting for
+//    chunk k-1: banded max-plus DP forgets its input, so after enough rows the
+//    guessed run equals the exact one up to one additive constant.  Those
+//    warm-up stripes write no cells; the run's state (H, F over the band) at the
+//    end of the warm-up and at the chunk's last row go to a checkpoint buffer,
+//    and chunk_check/chunk_add_kernel verify the constant exactly (every band
+//    entry) and add the prefix of the constants to each chunk's cells.  If any
+//    chunk has not converged, the plan's exact single-mode launch (queued
+//    behind, skipped otherwise) recomputes everything.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -146,11 +158,17 @@ struct KArgs {
   const int* border;         // pass-2 blocks in expected readiness order
   int brw, nseg, nblk;
   int nflow;                 // workgroups [0, nflow) run pass 1, the rest pass-2 blocks
+  // chunked banded mode (kp.single == 2)
+  int* ck;                   // [chunk][2: warm-up end, chunk end][2: H, F][ckw] band states
+  int ckw;                   // entries per band row (2*band + 1, padded)
+  const int* skip;           // exact single-mode launch: exit at once when *skip != 0
 };
 
 template <int ALG>
-__device__ __forceinline__ void border_top(const msa_kparams& kp, int c, int (&v)[3]) {
-  // Row 0 of the DP at column c (c may be < 0: unused, return NEG).
+__device__ __forceinline__ void border_top(const msa_kparams& kp, int c, int (&v)[3], int r0 = 0) {
+  // Row 0 of the DP at column c (c may be < 0: unused, return NEG).  Banded Gotoh,
+  // r0 > 0 (chunked mode): the GUESSED row r0 a chunk's warm-up starts from -- the
+  // row-0 border's tent moved to the diagonal, H = -h - g*|c - r0| inside the band.
   if constexpr (swlin(ALG)) {
     // G(0,c) = H(0,c) + g*c = g*c; SWL0 also on the virtual columns c < 0
     v[0] = (c >= 0 || ALG == MSA_ALG_SWL0) ? kp.gap_open * c : MSA_NEG;
@@ -161,9 +179,14 @@ __device__ __forceinline__ void border_top(const msa_kparams& kp, int c, int (&v
     v[1] = MSA_NEG;               // F
     v[2] = MSA_NEG;
   } else if constexpr (ALG == MSA_ALG_NWA) {
-    // H(0,c) = max(T1,T2,T3)(0,c): 0 at c=0, -h-g*c for 1<=c<=band; F = -inf
-    const bool inb = (kp.band < 0) || (c <= kp.band);
-    v[0] = (c == 0) ? 0 : ((c > 0 && inb) ? -kp.h - kp.gap_ext * c : MSA_NEG);
+    if (r0 > 0) {
+      const int d = c > r0 ? c - r0 : r0 - c;
+      v[0] = (d <= kp.band) ? -kp.h - kp.gap_ext * d : MSA_NEG;
+    } else {
+      // H(0,c) = max(T1,T2,T3)(0,c): 0 at c=0, -h-g*c for 1<=c<=band; F = -inf
+      const bool inb = (kp.band < 0) || (c <= kp.band);
+      v[0] = (c == 0) ? 0 : ((c > 0 && inb) ? -kp.h - kp.gap_ext * c : MSA_NEG);
+    }
     v[1] = MSA_NEG;
     v[2] = MSA_NEG;
   } else if constexpr (ALG == MSA_ALG_REF) {
@@ -514,6 +537,8 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
   const msa_kparams& kp = a.kp;
   const int lane = threadIdx.x & 63;
   const int w = uni(threadIdx.x >> 6);
+  // the exact launch queued behind a chunked run: nothing to do when every chunk converged
+  if (a.skip && uni(*(volatile const int*)a.skip)) return;
 
   // ---- LDS carve (int32 units, all offsets multiples of 4) ----
   int* misc = smem;  // 16 ints
@@ -541,13 +566,27 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
     if (item >= kp.n_items) break;
 
     int pair, k0, ns, group;
-    if (kp.single) {
+    int nwarm = 0;  // chunked: leading stripes of the item that only warm up (no cells, no meta)
+    if (kp.single == 1) {
       pair = 0;
       group = item;
       k0 = item * W;
       const msa_pair_desc pd0 = a.pairs[0];
       const int S = (pd0.m + 63) / 64;
       ns = min(W, S - k0);
+    } else if (kp.single == 2) {
+      pair = 0;
+      group = item;
+      const int S = (a.pairs[0].m + 63) / 64;
+      const int ks0 = item * kp.chunk_c;  // first stripe the chunk outputs
+      const int ke = min(S, ks0 + kp.chunk_c);
+      int kb = ks0 - kp.chunk_warm;
+      // a warm-up that would reach the matrix border (rows <= band + 64) starts at row 0
+      // instead, exactly: homogeneity (the guessed run = exact + constant) needs no border
+      if (kb * 64 <= kp.band + 64) kb = 0;
+      k0 = kb;
+      ns = ke - kb;
+      nwarm = ks0 - kb;
     } else {
       pair = item;
       group = 0;
@@ -674,7 +713,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
 
     if (w == W) {
       // =================== loader wave ===================
-      const bool act = kp.single && group > 0;
+      const bool act = kp.single == 1 && group > 0;
       StripeGeom s0 = sched[0];
       s0.cs = uni(s0.cs);
       s0.P = uni(s0.P);
@@ -685,13 +724,16 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
         chi = gp.c_hi;
       }
       const unsigned long long* g_in = act ? a.gbuf + (size_t)(group - 1) * NC * a.gbuf_stride : a.gbuf;
-      const bool border = (k0 == 0);  // the item holds the pair's first stripe: stage the DP's row 0
+      // the item holds the pair's first stripe: stage the DP's row 0; chunked: the guessed
+      // row above the chunk's first (warm-up) stripe
+      const bool border = (k0 == 0) || kp.single == 2;
+      const int brow = (kp.single == 2) ? 64 * k0 : 0;
       // all staging / sinking works in 16-column chunks; phase p = chunks [CPP*p, CPP*p + CPP)
       const int nch0 = s0.P * CPP;
       auto commit_border = [&](int c) __attribute__((always_inline)) {
         const int v = lane >> 4, l = lane & 15;
         int bv[3];
-        border_top<ALG>(kp, s0.cs + 16 * c + l, bv);
+        border_top<ALG>(kp, s0.cs + 16 * c + l, bv, brow);
         const int val = (v == 0) ? bv[0] : (v == 1 ? bv[1] : bv[2]);
         if (v < NC) stage[v * MSA_RING + ((16 * c + l) & (MSA_RING - 1))] = val;
       };
@@ -701,7 +743,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
       // one phase later (after the barrier that completes them).
       const int sl_idx = ns - 1;
       // (with the DPP shift register the compute wave publishes itself)
-      const bool sink = kp.single && (k0 + sl_idx) < S_pair - 1 && !(NC == 1 && SGL);
+      const bool sink = kp.single == 1 && (k0 + sl_idx) < S_pair - 1 && !(NC == 1 && SGL);
       StripeGeom sl = sched[sl_idx];
       sl.T = uni(sl.T); sl.P = uni(sl.P); sl.cs = uni(sl.cs);
       int sl_out_cs = 0;
@@ -883,7 +925,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
         in_ptr = rings + ((par_in * W + (w - 1)) * NC) * MSA_RING; in_vs = MSA_RING; in_mask = MSA_RING - 1;
       }
       int snk;
-      if (cur == ns - 1) snk = (kp.single && ks < S_pair - 1) ? SNK_GLOBAL : SNK_NONE;
+      if (cur == ns - 1) snk = (kp.single == 1 && ks < S_pair - 1) ? SNK_GLOBAL : SNK_NONE;
       else snk = (cur % W == W - 1) ? SNK_ROW : SNK_RING;
       int* const ring_out = rings + (((cur / W) & 1) * W + w) * NC * MSA_RING;
       int* out_ptr;
@@ -909,6 +951,18 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
       snk = uni(snk); out_cs = uni(out_cs); out_chi = uni(out_chi);
       unsigned long long* const g_out = a.gbuf + (size_t)group * NC * a.gbuf_stride;
       const size_t obase = (size_t)pd.out_off + (size_t)ks * pd.pmax * MSA_K * 64;  // pmax: 16-step blocks
+      // chunked mode: warm-up stripes store no cells and no meta (another chunk owns them);
+      // the warm-up's last stripe and the chunk's last stripe save lane 63's (H, F) row
+      const bool outp = uni(cur >= nwarm);
+      int ckslot = -1;
+      if constexpr (ALG == MSA_ALG_NWA) {
+        if (kp.single == 2) {
+          if (cur == nwarm - 1) ckslot = 2 * item;
+          else if (cur == ns - 1 && ks < S_pair - 1) ckslot = 2 * item + 1;
+        }
+      }
+      ckslot = uni(ckslot);
+      const int ckrow = 64 * ks + 64;  // lane 63's row
 
       // MASKED_: 0 no range checks; 1 per-lane start/end checks; 2..5 banded Gotoh in the
       // regular middle of the band, head (2, 3) or tail (4, 5) fix-ups by v_writelane, fix-up
@@ -1036,8 +1090,24 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
               }
             }
           }
+          if constexpr (ALG == MSA_ALG_NWA) {
+            // chunked mode: lane 63's band state of this quad into the checkpoint row (two
+            // stripes per chunk take this branch)
+            if (ckslot >= 0 && lane == 63) {
+#pragma unroll
+              for (int kk = 0; kk < 4; ++kk) {
+                const int col = sg.cs + KS * q + 4 * u + kk - 63;
+                const int e = col - (ckrow - kp.band);
+                if (e >= 0 && e <= 2 * kp.band && col >= 1 && col <= n) {
+                  a.ck[(size_t)(2 * ckslot) * a.ckw + e] = hist[0][4 * u + kk];
+                  a.ck[(size_t)(2 * ckslot + 1) * a.ckw + e] = hist[1][4 * u + kk];
+                }
+              }
+            }
+          }
           // cell outputs: one 1 KiB coalesced store per wave per 4 steps
-          if constexpr (OUT == MSA_OUT_H) {
+          if (!outp) {
+          } else if constexpr (OUT == MSA_OUT_H) {
             int4 h4;
             if constexpr (ALG == MSA_ALG_REF || ALG == MSA_ALG_PART) {
               h4 = make_int4(imax3(hist[0][4 * u], hist[1][4 * u], hist[2][4 * u]),
@@ -1056,7 +1126,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
             ntstore(t3row + u * 64, make_int4(hist[2][4 * u], hist[2][4 * u + 1], hist[2][4 * u + 2], hist[2][4 * u + 3]));
           }
         }
-        if constexpr (OUT == MSA_OUT_DIR) {
+        if (outp && OUT == MSA_OUT_DIR) {
 #pragma unroll
           for (int h = 0; h < CPP; ++h)
             ntstore(reinterpret_cast<int4*>(a.outDir + obase) + (size_t)(CPP * q + h) * 64 + lane,
@@ -1157,6 +1227,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
       ph += P;
       // ---- stripe finalize ----
       msa_stripe_meta* md = a.meta + pd.stripe0 + ks;
+      if (!outp) continue;  // a warm-up stripe: its meta belongs to the chunk that outputs it
       if constexpr (swlin(ALG) || ALG == MSA_ALG_SWA) {
         // first max in row-major order: max best, then min row
         const int bv = (TRACKPOS == 2) ? (L.best >> 15) : L.best;
@@ -1227,6 +1298,95 @@ struct PairResult {
   int32_t fin[3];
   int32_t pad;
 };
+
+// ---------------------------------------------------------------------------
+// Chunked banded mode (kp.single == 2), after the chunk launch.
+// chunk_check_kernel, one workgroup per chunk k >= 1: chunk k's run from its guessed
+// row reached the band row above its first output row with state (H, F) = `warm`;
+// chunk k-1 ended on the same row with `end`.  The guessed run is exact up to one
+// constant iff end - warm is the same number d_k at every finite entry and both are
+// -inf at the same entries (<= MSA_NEG/2: -inf may drift by a few gap costs).  Then
+// every later row of chunk k is its computed value + d_k (the recurrence is max-plus
+// homogeneous: it has no border term there) -- exact, not approximate.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void chunk_check_kernel(const int* __restrict__ ck, int ckw, int* dk, int* okk) {
+  const int k = blockIdx.x;
+  if (k == 0) {
+    if (threadIdx.x == 0) { dk[0] = 0; okk[0] = 1; }
+    return;
+  }
+  const int* end = ck + (size_t)(2 * (2 * (k - 1) + 1)) * ckw;  // slot 2(k-1)+1, planes H then F
+  const int* warm = ck + (size_t)(2 * (2 * k)) * ckw;           // slot 2k
+  __shared__ int first, bad;
+  if (threadIdx.x == 0) { first = 0x7fffffff; bad = 0; }
+  __syncthreads();
+  constexpr int NH = MSA_NEG / 2;
+  int mybad = 0;
+  for (int e = threadIdx.x; e < 2 * ckw; e += 256) {
+    const int x = end[e], y = warm[e];
+    if ((x > NH) != (y > NH)) mybad = 1;
+    else if (x > NH) atomicMin(&first, e);
+  }
+  if (mybad) atomicOr(&bad, 1);
+  __syncthreads();
+  const int f = first;
+  const int ref = (f < 2 * ckw) ? end[f] - warm[f] : 0;
+  mybad = (f >= 2 * ckw);  // no finite entry: nothing pins the constant
+  for (int e = threadIdx.x; e < 2 * ckw; e += 256) {
+    const int x = end[e], y = warm[e];
+    if (x > NH && x - y != ref) mybad = 1;
+  }
+  if (mybad) atomicOr(&bad, 1);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    dk[k] = ref;
+    okk[k] = bad ? 0 : 1;
+  }
+}
+
+// grid (x, n_chunks): chunk k adds e_k = d_1 + ... + d_k to the cells it output (stripes
+// [k*chunk_c, (k+1)*chunk_c), contiguous in the layout) and, for the stripe holding row m,
+// to the final state.  If any chunk did not converge nothing is added, *skip = 0 and the
+// tickets are reset: the exact single-mode launch queued next recomputes the pair.
+__global__ __launch_bounds__(256) void chunk_add_kernel(int32_t* H, const msa_pair_desc* pairs, msa_stripe_meta* meta,
+                                                        const int* dk, const int* okk, int n_chunks, int chunk_c,
+                                                        int* skip, int* ticket) {
+  const int k = blockIdx.y;
+  const msa_pair_desc pd = pairs[0];
+  const int S = (pd.m + 63) / 64;
+  __shared__ int sh_e, sh_ok;
+  if (threadIdx.x == 0) {
+    int e = 0, ok = 1;
+    for (int j = 0; j < n_chunks; ++j) {
+      ok &= okk[j];
+      if (j <= k) e += dk[j];
+    }
+    sh_e = e;
+    sh_ok = ok;
+    if (blockIdx.x == 0 && k == 0) {
+      *skip = ok;
+      if (!ok)
+        for (int t = 0; t < 16; ++t) ticket[t] = 0;
+    }
+    if (ok && blockIdx.x == 0 && k == n_chunks - 1) {
+      msa_stripe_meta* md = meta + pd.stripe0 + S - 1;
+#pragma unroll
+      for (int v = 0; v < 3; ++v)
+        if (md->fin[v] > MSA_NEG / 2) md->fin[v] += e;
+    }
+  }
+  __syncthreads();
+  const int e = sh_e;
+  if (!sh_ok || e == 0 || H == nullptr) return;
+  const int ks0 = k * chunk_c, ke = min(S, ks0 + chunk_c);
+  const size_t per = (size_t)pd.pmax * MSA_K * 64;  // int32 cells per stripe
+  int4* p = reinterpret_cast<int4*>(H + pd.out_off + (size_t)ks0 * per);
+  const size_t nv = (size_t)(ke - ks0) * per / 4;
+  for (size_t x = (size_t)blockIdx.x * 256 + threadIdx.x; x < nv; x += (size_t)gridDim.x * 256) {
+    const msa_v4i v = __builtin_nontemporal_load(reinterpret_cast<const msa_v4i*>(p + x));
+    __builtin_nontemporal_store(msa_v4i{v.x + e, v.y + e, v.z + e, v.w + e}, reinterpret_cast<msa_v4i*>(p + x));
+  }
+}
 
 __global__ __launch_bounds__(64) void reduce_pairs_kernel(const msa_pair_desc* pairs, const msa_stripe_meta* meta,
                                                          int n_pairs, int sw, PairResult* out) {

@@ -58,13 +58,18 @@ typedef struct msa_kparams {
   int32_t h;                // REF/NWA: h (border offsets)
   int32_t start_type;       // REF/PART start type
   int32_t band;             // -1: none, else |i-j| <= band
-  int32_t single;           // 1: one pair split in groups of WAVES stripes over workgroups
+  int32_t single;           // 1: one pair split in groups of WAVES stripes over workgroups;
+                            // 2: one banded pair in chunks of chunk_c stripes, one workgroup
+                            //    per chunk, each started chunk_warm stripes early from a guess
+                            //    (rank convergence, msa_kernels.hip)
   int32_t n_pairs;
   int32_t n_items;          // tickets
   uint32_t epoch;           // tag for cross-workgroup granules (nonzero, new per launch)
   int32_t sched_cap;        // stripes per item the LDS schedule can hold
   int32_t lds_code_bytes;   // per copy
   int32_t lds_row_words;    // wrap row buffer entries per carried value (batch mode)
+  int32_t chunk_c;          // single == 2: stripes each chunk outputs
+  int32_t chunk_warm;       // single == 2: warm-up stripes computed before a chunk's first one
 } msa_kparams;
 
 #ifdef __cplusplus

@@ -77,11 +77,30 @@ def c2_pair(rank: int = 0, synthetic: bool = False):
     return s[(rank + 1) % len(s)][:10000], s[0][:10000]
 
 
+def mutate(A: bytes, seed: int, sub: float = 0.01, indel: float = 0.001, max_indel: int = 8) -> bytes:
+    """A copy of A with i.i.d. substitutions (rate `sub`) and insertions / deletions of 1..max_indel
+    symbols (rate `indel`), positions and symbols from numpy's generator seeded with `seed`."""
+    rng = np.random.default_rng(seed)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    b = bytearray(A)
+    for k in rng.choice(len(b), size=int(len(b) * sub), replace=False):
+        b[k] = int(acgt[rng.integers(4)])
+    for k in sorted(rng.choice(len(b) - 2 * max_indel, size=int(len(b) * indel), replace=False), reverse=True):
+        ln = int(rng.integers(1, max_indel + 1))
+        if rng.integers(2):
+            del b[k:k + ln]
+        else:
+            b[k:k] = rng.choice(acgt, ln).tobytes()
+    return bytes(b)
+
+
 def c3_pair(synthetic: bool = False):
-    """C3: seq3 x seq4 truncated to 97,403 (band 512)."""
+    """C3: seq3 x seq4 truncated to 97,403 (band 512); synthetic: A = 100,000 i.i.d.
+    ACGT and B = A mutated (1% substitutions, 0.1% indels of 1..8), seed 0x5EED0003, B cut to 100,000."""
     if synthetic:
         A = synth(100000, 0x5EED0003)
-        return A, synth(100000, 0x5EED0003 + 1)
+        B = mutate(A, 0x5EED0003 + 1)[:100000]
+        return A, B
     s = bundled()
     return s[4][:C3_LEN], s[3][:C3_LEN]
 

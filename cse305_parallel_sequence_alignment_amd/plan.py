@@ -127,6 +127,14 @@ class Plan:
         LB.check(LB.lib().msa_plan_error(self._h, C.byref(v), _stream_ptr(stream)), "msa_plan_error")
         return int(v.value)
 
+    def run_info(self, stream=None) -> dict:
+        """How the last run was computed (msa_plan_run_info): launch mode, chunks, whether every chunk of a
+        chunked banded run converged (else the exact launch recomputed the cells), warm-up stripes."""
+        v = (C.c_int32 * 4)()
+        LB.check(LB.lib().msa_plan_run_info(self._h, v, _stream_ptr(stream)), "msa_plan_run_info")
+        return dict(mode={0: "stripe", 1: "flow", 2: "chunked"}[v[0]], chunks=int(v[1]), converged=int(v[2]),
+                    warm_stripes=int(v[3]))
+
     def clear_error(self, stream=None) -> None:
         LB.check(LB.lib().msa_plan_clear_error(self._h, _stream_ptr(stream)), "msa_plan_clear_error")
 

@@ -220,6 +220,12 @@ int msa_plan_run(msa_plan* plan, const uint8_t* dA, const uint8_t* dB, void* cel
  * msa_plan_clear_error) had a kernel wait hit its spin limit: the plan's error
  * word is sticky, so one check after many runs covers all of them. */
 int msa_plan_results(msa_plan* plan, msa_pair_result* out, void* stream);
+/* How the last run was computed: out4 = {launch mode (0 stripe kernel, 1 two-pass
+ * flow kernel, 2 chunked banded), chunks, converged (chunked: 1 = every chunk
+ * converged and the cells came from the chunk launch, 0 = the exact single-mode
+ * launch recomputed them; -1 otherwise), warm-up stripes per chunk}.
+ * Synchronizes `stream` for mode 2. */
+int msa_plan_run_info(msa_plan* plan, int32_t* out4, void* stream);
 /* The sticky error word (0 = no error; else the kernel site code), synchronizes. */
 int msa_plan_error(msa_plan* plan, int* code, void* stream);
 /* Reset the sticky error word (stream-ordered). */

@@ -461,6 +461,57 @@ def test_c3_full_size(oracle, dev, LB):
     score, digest = oracle.banded_ref(A, B, 512, 1.0, 2.0, want_digest=True)
     assert pl.results()[0]["score"] == int(score)
     assert pl.checksum(H) == digest
+    # the bench's pair converges in every chunk: the cells come from the chunked launch
+    assert pl.run_info() == dict(mode="chunked", chunks=pl.run_info()["chunks"], converged=1, warm_stripes=24)
+
+
+def _similar(rng, m, sub=0.02, indel=0.002):
+    """A random A and B = A with substitutions and short indels (length ~m)."""
+    A = rs(rng, m)
+    b = bytearray(A)
+    for k in rng.choice(m, size=int(m * sub), replace=False):
+        b[k] = ACGT[rng.integers(4)]
+    for k in sorted(rng.choice(m - 16, size=int(m * indel), replace=False), reverse=True):
+        if rng.integers(2):
+            del b[k:k + int(rng.integers(1, 8))]
+        else:
+            b[k:k] = rs(rng, int(rng.integers(1, 8)))
+    return A, bytes(b)
+
+
+@pytest.mark.parametrize("kind,m,w", [("similar", 12000, 512), ("similar", 20011, 256), ("similar", 9001, 64),
+                                      ("random", 12000, 512), ("similar_then_random", 16000, 512)])
+def test_banded_chunked(oracle, dev, LB, kind, m, w):
+    """Chunked banded runs (rank convergence): similar pairs converge in every chunk and the cells come from
+    the chunked launch plus the per-chunk constants; a random pair (or one whose second half is random) does
+    not, and the exact single-mode launch behind it recomputes the pair.  Either way the score and every
+    in-band H cell equal the banded oracle's, over repeated runs of the same plan."""
+    import torch
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+
+    rng = np.random.default_rng(m + w)
+    if kind == "random":
+        A, B = rs(rng, m), rs(rng, m + 37)
+    elif kind == "similar":
+        A, B = _similar(rng, m)
+    else:
+        A, B = _similar(rng, m // 2)
+        A, B = A + rs(rng, m - m // 2), B + rs(rng, m - m // 2)
+    if abs(len(A) - len(B)) > w:
+        B = B[:len(A) + w // 2]
+    pl = Plan(LB.NW_BANDED, LB.CELLS_H, [len(A)], [len(B)], [0], [0], match=1, mismatch=0, gap_open=3,
+              gap_extend=1, band=w)
+    H = torch.empty(pl.cells_elems, dtype=torch.int32, device=dev)
+    score, digest = oracle.banded_ref(A, B, w, 1.0, 2.0, want_digest=True)
+    for _ in range(2):
+        H.fill_(7)
+        pl.run(_dev(A, dev), _dev(B, dev), H)
+        assert pl.results()[0]["score"] == int(score)
+        assert pl.checksum(H) == digest
+        info = pl.run_info()
+        assert info["mode"] == "chunked" and info["chunks"] >= 4
+        assert info["converged"] == (1 if kind == "similar" else 0), info
+    assert pl.error() == 0
 
 
 def _rescore(A, B, beg, cigar, ma, mi, go, ge):
