@@ -60,9 +60,9 @@ def main_alignment_text(A: bytes, B: bytes, m: int, n: int, p: int = 32, g: floa
     L = LB.lib()
     need = C.c_size_t()
     score = C.c_double()
-    LB.check(L.msa_main_alignment(A, B, m, n, p, g, h, None, 0, C.byref(need), None), "msa_main_alignment")
-    buf = C.create_string_buffer(need.value + 1)
-    LB.check(L.msa_main_alignment(A, B, m, n, p, g, h, buf, need.value + 1, C.byref(need), C.byref(score)),
+    # five progress lines + two alignment lines of at most m+n characters: one call fits
+    buf = C.create_string_buffer(64 + 2 * (m + n + 2))
+    LB.check(L.msa_main_alignment(A, B, m, n, p, g, h, buf, len(buf), C.byref(need), C.byref(score)),
              "msa_main_alignment")
     return buf.raw[:need.value].decode("latin-1"), score.value
 
