@@ -15,6 +15,7 @@
 #include <string>
 #include <thread>
 #include <map>
+#include <tuple>
 #include <vector>
 
 #include "../../include/msa.h"
@@ -218,6 +219,37 @@ int nc_of(int alg) {
 }
 
 typedef void (*kfn_t)(KArgs);
+
+// Per-process caches of what plan creation asks the runtime: compute units per device
+// (hipGetDeviceProperties is slow, and main_alignment_function creates a plan per call)
+// and, per (device, kernel, block, LDS), the dynamic-LDS attribute and the occupancy.
+std::mutex g_shape_mu;
+int device_cus() {
+  static std::map<int, int> cus;
+  const int dev = current_device();
+  std::lock_guard<std::mutex> lk(g_shape_mu);
+  auto it = cus.find(dev);
+  if (it != cus.end()) return it->second;
+  hipDeviceProp_t prop;
+  const int n = (hipGetDeviceProperties(&prop, dev) == hipSuccess) ? prop.multiProcessorCount : 1;
+  cus[dev] = n;
+  return n;
+}
+// sets the kernel's dynamic-LDS limit and returns its occupancy (blocks per CU, >= 1), or -1
+int kernel_shape(kfn_t fn, int threads, size_t lds) {
+  static std::map<std::tuple<int, kfn_t, int, size_t>, int> occ_of;
+  const auto key = std::make_tuple(current_device(), fn, threads, lds);
+  std::lock_guard<std::mutex> lk(g_shape_mu);
+  auto it = occ_of.find(key);
+  if (it != occ_of.end()) return it->second;
+  if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return -1;
+  int occ = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)fn, threads, lds) != hipSuccess || occ < 1)
+    occ = 1;
+  occ_of[key] = occ;
+  return occ;
+}
 
 // single-pair phase length: 32 steps for one carried value (SW linear); 16 when
 // two or three values per cell are carried (register pressure: no spills)
@@ -575,27 +607,20 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     delete P;
     return MSA_ERR_UNSUPPORTED;
   }
-  if (hipFuncSetAttribute((const void*)P->fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P->lds_bytes) !=
-      hipSuccess) {
+  const int occ = kernel_shape(P->fn, P->threads, P->lds_bytes);
+  if (occ < 0) {
     delete P;
     return MSA_ERR_HIP;
   }
-  int occ = 1;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)P->fn, P->threads, P->lds_bytes) !=
-          hipSuccess || occ < 1)
-    occ = 1;
-  hipDeviceProp_t prop;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  (void)hipGetDeviceProperties(&prop, dev);
-  const int cap = prop.multiProcessorCount * std::min(occ, 2);
+  const int ncu = device_cus();
+  const int cap = ncu * std::min(occ, 2);
   P->grid = std::max(1, std::min(kp.n_items, cap));
   if (flow) {
     // items in 8 contiguous chunks, one per XCD (workgroup b takes tickets of chunk b % 8,
     // round-robin placement puts it on XCD b % 8): consecutive items hand off inside one
     // L2 except at 7 chunk seams.  Speed only: an item only waits on an earlier one and
     // every workgroup is resident (one per CU, grid <= CUs), whatever the placement.
-    const int per_xcd = std::max(1, prop.multiProcessorCount / 8);
+    const int per_xcd = std::max(1, ncu / 8);
     const int chunk = (kp.n_items + 7) / 8;
     kp.sched_cap = chunk;
     P->grid = 8 * std::max(1, std::min(chunk, per_xcd));
@@ -607,10 +632,16 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   // launch is one long chain of ~S x 8 phases.  Chunked mode runs it as n_chunks
   // independent chains of chunk_c (+ warm-up) stripes at once (rank convergence,
   // msa_kernels.hip header), with the exact launch kept behind it as the fallback.
-  constexpr int kWarm = 24;  // warm-up stripes (1,536 rows): C3's pair converges within ~900
+#ifndef MSA_CHUNK_WARM
+#define MSA_CHUNK_WARM 24  // warm-up stripes (1,536 rows): C3's pair converges within ~900
+#endif
+#ifndef MSA_CHUNK_MIN
+#define MSA_CHUNK_MIN 24   // stripes per chunk, at least
+#endif
+  constexpr int kWarm = MSA_CHUNK_WARM;
   if (single && kalg == MSA_ALG_NWA && band >= 0 && (out_mode == MSA_OUT_H || out_mode == MSA_OUT_NONE)) {
     const int S = (int)((desc->m[0] + 63) / 64);
-    const int cc = std::max(kWarm, (S + prop.multiProcessorCount - 1) / prop.multiProcessorCount);
+    const int cc = std::max(MSA_CHUNK_MIN, (S + ncu - 1) / ncu);
     const int nch = (S + cc - 1) / cc;
     kfn_t cfn = pick_kernel(kalg, out_mode, 0, false);
     if (nch >= 4 && cfn) {
@@ -632,18 +663,13 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
       P->threads = (MSA_WAVES_BATCH + 1) * 64;
       P->lds_bytes = (16 + (size_t)kp.sched_cap * 8 + (size_t)(2 * MSA_WAVES_BATCH + 1) * P->nc * MSA_RING +
                       (size_t)P->nc * kp.lds_row_words) * 4;
-      if (P->lds_bytes > 160 * 1024 ||
-          hipFuncSetAttribute((const void*)P->fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P->lds_bytes) !=
-              hipSuccess) {
+      const int occ2 = (P->lds_bytes > 160 * 1024) ? -1 : kernel_shape(P->fn, P->threads, P->lds_bytes);
+      if (occ2 < 0) {
         delete P;
         return MSA_ERR_UNSUPPORTED;
       }
-      int occ2 = 1;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ2, (const void*)P->fn, P->threads, P->lds_bytes) !=
-              hipSuccess || occ2 < 1)
-        occ2 = 1;
       // every chunk at once (one workgroup each); more chunks than slots just queue
-      P->grid = std::max(1, std::min(nch, prop.multiProcessorCount * std::min(occ2, 2)));
+      P->grid = std::max(1, std::min(nch, ncu * std::min(occ2, 2)));
       P->ckw = (2 * band + 1 + 3) & ~3;
     }
   }
