@@ -375,9 +375,115 @@ int orc_partial_tables(const char* A, const char* B, uint64_t m, uint64_t n, dou
   return ORC_OK;
 }
 
-/* findPartitionParallel (partial.cpp:81-146); out receives p+1 nodes
- * (sorted by (i,j) with a stable sort; the reference's std::sort is an
- * insertion sort -- hence stable -- for the <=16 elements of every p<=15). */
+/* The reference sorts its partition with std::sort (partial.cpp:141-143), which is not
+ * stable for more than 16 elements: points with equal (i, j) -- e.g. the (0,0,0) a band
+ * with no cell above INT_MIN contributes when p > m -- come out in introsort's order.
+ * This restates libstdc++'s std::sort (bits/stl_algo.h, stl_heap.h: introsort loop with
+ * depth limit 2*floor(log2 n), median-of-three pivot moved to the first element,
+ * unguarded Hoare partition, heapsort when the depth limit runs out, then insertion
+ * sort of the first 16 and unguarded insertion of the rest) for the reference's
+ * comparator (a.i < b.i || (a.i == b.i && a.j < b.j)); pinned by partial_ties.json,
+ * which the reference's own build produced. */
+static int orc_less(const orc_node* a, const orc_node* b) { return a->i < b->i || (a->i == b->i && a->j < b->j); }
+static void orc_swap(orc_node* a, orc_node* b) { orc_node t = *a; *a = *b; *b = t; }
+static void orc_push_heap(orc_node* f, long hole, long top, orc_node v) {
+  long parent = (hole - 1) / 2;
+  while (hole > top && orc_less(&f[parent], &v)) { f[hole] = f[parent]; hole = parent; parent = (hole - 1) / 2; }
+  f[hole] = v;
+}
+static void orc_adjust_heap(orc_node* f, long hole, long len, orc_node v) {
+  const long top = hole;
+  long second = hole;
+  while (second < (len - 1) / 2) {
+    second = 2 * (second + 1);
+    if (orc_less(&f[second], &f[second - 1])) second--;
+    f[hole] = f[second];
+    hole = second;
+  }
+  if ((len & 1) == 0 && second == (len - 2) / 2) {
+    second = 2 * (second + 1);
+    f[hole] = f[second - 1];
+    hole = second - 1;
+  }
+  orc_push_heap(f, hole, top, v);
+}
+static void orc_heap_sort(orc_node* f, long len) {
+  if (len >= 2)  /* make_heap */
+    for (long parent = (len - 2) / 2;; parent--) {
+      orc_adjust_heap(f, parent, len, f[parent]);
+      if (parent == 0) break;
+    }
+  for (long last = len; last > 1;) {  /* sort_heap: pop_heap */
+    last--;
+    const orc_node v = f[last];
+    f[last] = f[0];
+    orc_adjust_heap(f, 0, last, v);
+  }
+}
+static void orc_median_to_first(orc_node* r, orc_node* a, orc_node* b, orc_node* c) {
+  if (orc_less(a, b)) {
+    if (orc_less(b, c)) orc_swap(r, b);
+    else if (orc_less(a, c)) orc_swap(r, c);
+    else orc_swap(r, a);
+  } else if (orc_less(a, c)) orc_swap(r, a);
+  else if (orc_less(b, c)) orc_swap(r, c);
+  else orc_swap(r, b);
+}
+static orc_node* orc_unguarded_partition(orc_node* first, orc_node* last, const orc_node* pivot) {
+  for (;;) {
+    while (orc_less(first, pivot)) ++first;
+    --last;
+    while (orc_less(pivot, last)) --last;
+    if (!(first < last)) return first;
+    orc_swap(first, last);
+    ++first;
+  }
+}
+static void orc_introsort_loop(orc_node* first, orc_node* last, long depth) {
+  while (last - first > 16) {
+    if (depth == 0) { orc_heap_sort(first, last - first); return; }
+    --depth;
+    orc_node* mid = first + (last - first) / 2;
+    orc_median_to_first(first, first + 1, mid, last - 1);
+    orc_node* cut = orc_unguarded_partition(first + 1, last, first);
+    orc_introsort_loop(cut, last, depth);
+    last = cut;
+  }
+}
+static void orc_unguarded_linear_insert(orc_node* last) {
+  const orc_node v = *last;
+  orc_node* next = last - 1;
+  while (orc_less(&v, next)) { *last = *next; last = next; --next; }
+  *last = v;
+}
+static void orc_insertion_sort(orc_node* first, orc_node* last) {
+  if (first == last) return;
+  for (orc_node* i = first + 1; i != last; ++i) {
+    if (orc_less(i, first)) {
+      const orc_node v = *i;
+      memmove(first + 1, first, (size_t)(i - first) * sizeof(orc_node));
+      *first = v;
+    } else {
+      orc_unguarded_linear_insert(i);
+    }
+  }
+}
+void orc_std_sort(orc_node* first, uint64_t count) {
+  orc_node* last = first + count;
+  if (count < 2) return;
+  long lg = 0;
+  for (uint64_t x = count; x > 1; x >>= 1) lg++;
+  orc_introsort_loop(first, last, 2 * lg);
+  if (last - first > 16) {
+    orc_insertion_sort(first, first + 16);
+    for (orc_node* i = first + 16; i != last; ++i) orc_unguarded_linear_insert(i);
+  } else {
+    orc_insertion_sort(first, last);
+  }
+}
+
+/* findPartitionParallel (partial.cpp:81-146); out receives p+1 nodes sorted as the
+ * reference's std::sort leaves them (orc_std_sort). */
 int orc_partial_partition(const int32_t* T1, const int32_t* T2, const int32_t* T3, const int32_t* R1,
                           const int32_t* R2, const int32_t* R3, uint64_t m, uint64_t n, uint64_t p,
                           double h, orc_node* out, uint64_t cap, uint64_t* n_out) {
@@ -411,16 +517,7 @@ int orc_partial_partition(const int32_t* T1, const int32_t* T2, const int32_t* T
 #undef VAL
 #undef TYPE
   out[cnt].i = m; out[cnt].j = n; out[cnt].t = 1; out[cnt].pad = 0; cnt++;
-  /* stable insertion sort by (i, j) */
-  for (uint64_t a = 1; a < cnt; a++) {
-    orc_node key = out[a];
-    uint64_t b = a;
-    while (b > 0 && ((key.i < out[b - 1].i) || (key.i == out[b - 1].i && key.j < out[b - 1].j))) {
-      out[b] = out[b - 1];
-      b--;
-    }
-    out[b] = key;
-  }
+  orc_std_sort(out, cnt);  /* partial.cpp:141-143 */
   *n_out = cnt;
   return ORC_OK;
 }

@@ -169,8 +169,37 @@ def main():
     print("wrote fixtures to", HERE)
 
 
+def partial_ties():
+    """partial_ties.json: partitions with p >= 16 whose points tie on (i, j) (bands with no cell above
+    INT_MIN give (0,0,0) when p > m or p > n; equal winners of different bands), so the reference's
+    std::sort (partial.cpp:141-143, introsort: not stable past 16 elements) fixes their order."""
+    rng = np.random.default_rng(0x5EED0016)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    out = []
+    for (m, n) in [(5, 5), (10, 30), (30, 10), (15, 15), (20, 20), (12, 40), (40, 12), (64, 64), (3, 200),
+                   (100, 100)]:
+        for p in (16, 17, 20, 24, 32, 40, 64):
+            for st, et in ((-1, -1), (1, 1), (2, 3), (3, -1)):
+                A, B = rng.choice(acgt, m).tobytes(), rng.choice(acgt, n).tobytes()
+                g, h = GH[len(out) % len(GH)]
+                part = O.ref_partial(A, B, p, g, h, st, et)
+                keys = [(i, j) for (i, j, _) in part]
+                if len(set(keys)) == len(keys):
+                    continue  # no tie: nothing the sort order decides
+                # a stable sort keeps the input order among ties: (0,0,-1) pushed first stays first among
+                # the (0,0,*) points and (m,n,1) pushed last stays last among the (m,n,*) ones
+                z = [t for (i, j, t) in part if (i, j) == (0, 0)]
+                e = [t for (i, j, t) in part if (i, j) == (m, n)]
+                out.append(dict(A=A.decode(), B=B.decode(), p=p, g=g, h=h, start=st, end=et, partition=part,
+                                differs_from_stable=bool(z[0] != -1 or e[-1] != 1)))
+    (HERE / "partial_ties.json").write_text(json.dumps(out))
+    print("partial_ties:", len(out), "cases,", sum(c["differs_from_stable"] for c in out), "differ from a stable sort")
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["at_size"]:
         at_size()
+    elif sys.argv[1:] == ["partial_ties"]:
+        partial_ties()
     else:
         main()

@@ -234,6 +234,18 @@ def test_partial_fixtures(oracle, dev, dataset):
         assert np.array_equal(a, b)
 
 
+def test_partial_partition_tie_order(dev):
+    """findPartialBalancedPartitionParallel with p >= 16 on the GPU: points tying on (i, j) in the order
+    of the reference's std::sort (partial.cpp:141-143), all 116 fixtures of partial_ties.json."""
+    from cse305_parallel_sequence_alignment_amd import api
+
+    for c in json.loads((GOLDEN / "partial_ties.json").read_text()):
+        A, B = c["A"].encode(), c["B"].encode()
+        got = [a.as_tuple() for a in api.findPartialBalancedPartitionParallel(A, B, len(A), len(B), c["p"], c["g"],
+                                                                               c["h"], c["start"], c["end"])]
+        assert got == [tuple(x) for x in c["partition"]], (c["p"], len(A), len(B))
+
+
 def test_sw_affine_traceback(oracle, dev):
     from cse305_parallel_sequence_alignment_amd import api
 

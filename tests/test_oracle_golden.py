@@ -81,6 +81,19 @@ def test_partial_partition(oracle, k):
     assert got == [tuple(x) for x in c["partition"]]
 
 
+TIES = json.loads((GOLDEN / "partial_ties.json").read_text())
+
+
+def test_partial_partition_tie_order(oracle):
+    """p >= 16: points that tie on (i, j) come out in the order of the reference's std::sort (introsort,
+    not stable past 16 elements); 104 of the 116 fixtures differ from what a stable sort gives."""
+    assert sum(c["differs_from_stable"] for c in TIES) > 50
+    for c in TIES:
+        got = oracle.partial_partition(c["A"].encode(), c["B"].encode(), c["p"], c["g"], c["h"], c["start"],
+                                       c["end"])
+        assert got == [tuple(x) for x in c["partition"]], (c["p"], len(c["A"]), len(c["B"]))
+
+
 @pytest.mark.skipif("not __import__('oracle.oracle', fromlist=['x']).ref_available()",
                     reason="oracle/_ref not built (reference sources absent)")
 def test_restatement_vs_reference_live(oracle):
@@ -96,6 +109,8 @@ def test_restatement_vs_reference_live(oracle):
         assert [tuple(x) for x in r["nodes"]] == [tuple(x) for x in ref["nodes"]]
         p = int(rng.integers(1, 6))
         assert oracle.partial_partition(A, B, p, 1.0, 2.0, 1, 1) == oracle.ref_partial(A, B, p, 1.0, 2.0, 1, 1)
+        p = int(rng.integers(16, 90))  # introsort territory (std::sort past 16 elements)
+        assert oracle.partial_partition(A, B, p, 1.0, 2.0, -1, -1) == oracle.ref_partial(A, B, p, 1.0, 2.0, -1, -1)
 
 
 def test_oracle_at_size_10k(oracle, dataset):
