@@ -213,7 +213,7 @@ StreamPool& stream_pool() {
 int nc_of(int alg) {
   switch (alg) {
     case MSA_ALG_SWL: case MSA_ALG_SWL0: return 1;
-    case MSA_ALG_SWA: case MSA_ALG_NWA: return 2;
+    case MSA_ALG_SWA: case MSA_ALG_NWA: case MSA_ALG_REF1: return 2;
     default: return 3;
   }
 }
@@ -287,6 +287,10 @@ kfn_t pick_kernel(int alg, int out, int tp, bool sgl) {
       if (out == MSA_OUT_TAB) return kf<MSA_ALG_REF, MSA_OUT_TAB, 0>(sgl);
       if (out == MSA_OUT_DIR) return kf<MSA_ALG_REF, MSA_OUT_DIR, 0>(sgl);
       if (out == MSA_OUT_H) return kf<MSA_ALG_REF, MSA_OUT_H, 0>(sgl);
+      break;
+    case MSA_ALG_REF1:
+      if (out == MSA_OUT_NONE) return kf<MSA_ALG_REF1, MSA_OUT_NONE, 0>(sgl);
+      if (out == MSA_OUT_DIR) return kf<MSA_ALG_REF1, MSA_OUT_DIR, 0>(sgl);
       break;
     case MSA_ALG_PART:
       if (out == MSA_OUT_TAB) return kf<MSA_ALG_PART, MSA_OUT_TAB, 0>(sgl);
@@ -452,7 +456,17 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
       break;
     case MSA_SW_AFFINE: kalg = MSA_ALG_SWA; break;
     case MSA_NW_BANDED: kalg = MSA_ALG_NWA; break;
-    case MSA_REF_GOTOH: kalg = MSA_ALG_REF; break;
+    case MSA_REF_GOTOH: {
+      // start type -1 (main_alignment_function's single subproblem) with direction bytes or no
+      // cells: the tagged-max form (every interior value is finite; values carried x4)
+      int64_t span = 0;
+      for (int64_t p = 0; p < desc->n_pairs; ++p) span = std::max(span, desc->m[p] + desc->n[p] + 2);
+      const bool ref1 = desc->start_type == -1 && (out_mode == MSA_OUT_DIR || out_mode == MSA_OUT_NONE) &&
+                        desc->gap_extend >= 0 && desc->gap_open >= desc->gap_extend &&
+                        (int64_t)4 * (desc->gap_open + 1) * span < (int64_t(1) << 28);
+      kalg = ref1 ? MSA_ALG_REF1 : MSA_ALG_REF;
+      break;
+    }
     case MSA_PARTIAL: kalg = MSA_ALG_PART; break;
     default: delete P; return MSA_ERR_ARG;
   }
@@ -943,7 +957,8 @@ int msa_plan_traceback(msa_plan* P, int64_t pair, const uint8_t* dDir, uint8_t* 
   hipStream_t st = (hipStream_t)stream;
   P->note_stream(st);
   hipLaunchKernelGGL(traceback_kernel<false>, dim3(1), dim3(64), 0, st, dDir, P->d_pairs, P->d_meta,
-                     (const PairResult*)P->d_res, (int)pair, 0, 0, d_ops, (long long)ops_cap, (long long*)d_info);
+                     (const PairResult*)P->d_res, (int)pair, 0, 0, 0, d_ops, (long long)ops_cap,
+                     (long long*)d_info);
   HIPCHK(hipGetLastError());
   return MSA_OK;
 }
@@ -952,12 +967,14 @@ int msa_plan_traceback_gotoh(msa_plan* P, int64_t pair, int end_type, const uint
                              int64_t ops_cap, int64_t* d_info, void* stream) {
   if (!P || !dDir || !d_ops || !d_info || ops_cap < 0 || pair < 0 || pair >= P->d.n_pairs) return MSA_ERR_ARG;
   if (end_type < -3 || end_type > 3 || end_type == 0) return MSA_ERR_ARG;
-  if (P->kp.alg != MSA_ALG_REF || P->d.cells != MSA_CELLS_DIR) return MSA_ERR_UNSUPPORTED;
+  if ((P->kp.alg != MSA_ALG_REF && P->kp.alg != MSA_ALG_REF1) || P->d.cells != MSA_CELLS_DIR)
+    return MSA_ERR_UNSUPPORTED;
   hipStream_t st = (hipStream_t)stream;
   P->note_stream(st);
+  // REF1 bytes hold tags (3 / 2 / 1 = T1 / T2 / T3), REF bytes the table numbers
   hipLaunchKernelGGL(traceback_kernel<true>, dim3(1), dim3(64), 0, st, dDir, P->d_pairs, P->d_meta,
-                     (const PairResult*)P->d_res, (int)pair, end_type, (int)P->kp.h, d_ops, (long long)ops_cap,
-                     (long long*)d_info);
+                     (const PairResult*)P->d_res, (int)pair, end_type, (int)P->kp.h,
+                     P->kp.alg == MSA_ALG_REF1 ? 1 : 0, d_ops, (long long)ops_cap, (long long*)d_info);
   HIPCHK(hipGetLastError());
   return MSA_OK;
 }

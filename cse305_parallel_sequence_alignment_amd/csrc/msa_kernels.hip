@@ -82,6 +82,7 @@ constexpr bool swlin(int alg) { return alg == MSA_ALG_SWL || alg == MSA_ALG_SWL0
 template <> struct Tr<MSA_ALG_SWA> { static constexpr int NC = 2; };
 template <> struct Tr<MSA_ALG_NWA> { static constexpr int NC = 2; };
 template <> struct Tr<MSA_ALG_REF> { static constexpr int NC = 3; };
+template <> struct Tr<MSA_ALG_REF1> { static constexpr int NC = 2; };
 template <> struct Tr<MSA_ALG_PART> { static constexpr int NC = 3; };
 
 __device__ __forceinline__ int dpp_shr1(int old, int src) {
@@ -189,6 +190,20 @@ __device__ __forceinline__ void border_top(const msa_kparams& kp, int c, int (&v
     }
     v[1] = MSA_NEG;
     v[2] = MSA_NEG;
+  } else if constexpr (ALG == MSA_ALG_REF1) {
+    // row 0 for start type -1 (:212-227): T1(0,0) = 0, T2(0,c) = -h-g*c (c >= 1), rest -inf;
+    // tagged (see step<REF1>): v[0] = max(T1,T2,T3)~, v[1] = the row below's T3 candidates~
+    const int GH = kp.gap_open, G = kp.gap_ext;
+    if (c < 0) { v[0] = v[1] = v[2] = MSA_NEG; return; }
+    if (c == 0) {
+      v[0] = 3;                // T1 = 0, tag T1
+      v[1] = 4 * (-GH) + 3;    // T1 - g - h
+    } else {
+      const int t2 = -kp.h - G * c;
+      v[0] = 4 * t2 + 2;
+      v[1] = 4 * (t2 - GH) + 2;
+    }
+    v[2] = MSA_NEG;
   } else if constexpr (ALG == MSA_ALG_REF) {
     // compute_row(0) / ComputeFirstRowMapThread (subproblem_alignment.cpp:212-227,259-280)
     const int st = kp.start_type;
@@ -227,6 +242,12 @@ __device__ __forceinline__ void border_left(const msa_kparams& kp, int i, int (&
     v[0] = inb ? -kp.h - kp.gap_ext * i : MSA_NEG;  // H
     v[1] = MSA_NEG;                                 // T2 (E)
     v[2] = v[0];                                    // T3 (F) = -h-g*i
+  } else if constexpr (ALG == MSA_ALG_REF1) {
+    // column 0 for start type -1 (:282-292): T1 = T2 = -inf, T3 = -h-g*i; state (H~, R~, D~)
+    const int t3 = -kp.h - kp.gap_ext * i;
+    v[0] = 4 * t3 + 1;
+    v[1] = 4 * (t3 - kp.gap_open) + 1;
+    v[2] = 4 * (t3 - kp.gap_ext) + 1;
   } else if constexpr (ALG == MSA_ALG_REF) {
     // compute_row(i>0) borders (subproblem_alignment.cpp:282-292)
     const int st = kp.start_type;
@@ -271,6 +292,7 @@ __device__ __forceinline__ unsigned step(const msa_kparams& kp, LaneState<ALG>& 
                                          int t, int ct, int (&carry)[3], int& hout) {
   unsigned dir = 0;
   int nS[3];
+  int fin_tab[3];  // REF1: the cell's untagged T1, T2, T3 (the final state at (m, n))
   if constexpr (ALG == MSA_ALG_SWL) {
     // ct = g*(i+j) is the same for every lane (one anti-diagonal): an SGPR
     const int up = dpp_shr1(in[0], L.S[0]);
@@ -316,6 +338,33 @@ __device__ __forceinline__ unsigned step(const msa_kparams& kp, LaneState<ALG>& 
     nS[1] = t2;
     nS[2] = t3;
     L.U[0] = upH;
+  } else if constexpr (ALG == MSA_ALG_REF1) {
+    // Start type -1: every table value of every cell with i, j >= 1 is finite (each has a
+    // finite predecessor), so -inf needs no exact emulation and the three first-maximum
+    // selections of find_alignment (:130-145) fold into the maxima: a value of table k is
+    // carried TAGGED as 4*T + (4-k), so max() of tagged values is the maximum, ties going to
+    // the lower table -- the reference's order.  Per cell the lane forms
+    //   H~ = max(T1~, T2~, T3~)            -> the cell diagonally below: T1 = H + f, its tag
+    //   R~ = max(T1~ - 4gh, T2~ - 4g, T3~ - 4gh)  (gh = g + h) -> T2 of the cell to the right
+    //   D~ = max(T1~ - 4gh, T2~ - 4gh, T3~ - 4g)  -> T3 of the cell below
+    // so only H~ and D~ cross lanes (2 DPPs), and the direction byte is three tags: the
+    // diagonal's H~ (T1's predecessor), the left cell's R~ (T2's), the upper cell's D~ (T3's);
+    // tag 3 / 2 / 1 = table T1 / T2 / T3.  s = 4f (profile).
+    const int uH = dpp_shr1(in[0], L.S[0]);
+    const int uD = dpp_shr1(in[1], L.S[2]);
+    const int GH4 = 4 * kp.gap_open, G4 = 4 * kp.gap_ext;
+    const int t1 = (int)((unsigned)L.U[0] | 3u) + s;  // 4(H_diag + f) + 3
+    const int t2 = (int)(((unsigned)L.S[1] & ~3u) | 2u);
+    const int t3 = (int)(((unsigned)uD & ~3u) | 1u);
+    nS[0] = imax3(t1, t2, t3);
+    nS[1] = imax(imax(t1, t3) - GH4, t2 - G4);
+    nS[2] = imax(imax(t1, t2) - GH4, t3 - G4);
+    if constexpr (OUT == MSA_OUT_DIR)
+      dir = ((unsigned)L.U[0] & 3u) | (((unsigned)L.S[1] & 3u) << 2) | (((unsigned)uD & 3u) << 4);
+    fin_tab[0] = t1 >> 2;
+    fin_tab[1] = t2 >> 2;
+    fin_tab[2] = t3 >> 2;
+    L.U[0] = uH;
   } else if constexpr (ALG == MSA_ALG_REF) {
     const int u0 = dpp_shr1(in[0], L.S[0]);
     const int u1 = dpp_shr1(in[1], L.S[1]);
@@ -351,6 +400,7 @@ __device__ __forceinline__ unsigned step(const msa_kparams& kp, LaneState<ALG>& 
     L.U[2] = u2;
   }
   constexpr int NS = swlin(ALG) ? 1 : 3;
+  (void)fin_tab;
   if constexpr (MASKED) {
     const bool before = t < L.tmin;
     const bool after = t > L.tmax;
@@ -371,7 +421,7 @@ __device__ __forceinline__ unsigned step(const msa_kparams& kp, LaneState<ALG>& 
     } else if constexpr (FIN) {  // only the stripe holding row m
       if (t == L.tmax) {
 #pragma unroll
-        for (int v = 0; v < 3; ++v) L.fin[v] = nS[v];
+        for (int v = 0; v < 3; ++v) L.fin[v] = (ALG == MSA_ALG_REF1) ? fin_tab[v] : nS[v];
       }
     }
   } else {
@@ -392,7 +442,7 @@ __device__ __forceinline__ unsigned step(const msa_kparams& kp, LaneState<ALG>& 
   // carried values (what the lane below / next stripe needs)
   if constexpr (swlin(ALG)) {
     carry[0] = nS[0];
-  } else if constexpr (ALG == MSA_ALG_SWA || ALG == MSA_ALG_NWA) {
+  } else if constexpr (ALG == MSA_ALG_SWA || ALG == MSA_ALG_NWA || ALG == MSA_ALG_REF1) {
     carry[0] = nS[0];
     carry[1] = nS[2];
   } else {
@@ -868,6 +918,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
       {
         int sm, sx;
         if constexpr (ALG == MSA_ALG_REF || ALG == MSA_ALG_NWA) { sm = 1; sx = 0; }
+        else if constexpr (ALG == MSA_ALG_REF1) { sm = 4; sx = 0; }  // 4f: tagged values
         else if constexpr (ALG == MSA_ALG_PART) { sm = 0; sx = 1; }
         else if constexpr (swlin(ALG)) { sm = kp.match + 2 * kp.gap_open; sx = kp.mismatch + 2 * kp.gap_open; }
         else { sm = kp.match; sx = kp.mismatch; }

@@ -97,7 +97,7 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
                                                        const msa_pair_desc* __restrict__ pairs,
                                                        const msa_stripe_meta* __restrict__ meta,
                                                        const PairResult* __restrict__ res, int pair, int end_type,
-                                                       int hpen, uint8_t* __restrict__ ops, long long cap,
+                                                       int hpen, int tagdir, uint8_t* __restrict__ ops, long long cap,
                                                        long long* __restrict__ info) {
   const int lane = threadIdx.x;
   const msa_pair_desc pd = pairs[pair];
@@ -269,7 +269,11 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
         if constexpr (REF) {
           // table s (T1, T2, T3) leaves by its fixed move (diagonal 9, left 1, up 8) into the
           // table bits 2s..2s+1 name; 0 there (no predecessor) stops the walk with an error
-          auto fld = [](unsigned step, unsigned nt) { return step | ((nt ? 9u * (nt - 1u) : 27u) << 4); };
+          // (tagdir: the tagged-max fill stores tag 4 - table; 0 stays "no predecessor")
+          auto fld = [&](unsigned step, unsigned x) {
+            const unsigned nt = (tagdir && x) ? 4u - x : x;
+            return step | ((nt ? 9u * (nt - 1u) : 27u) << 4);
+          };
           wt = (int)(fld(9u, dv & 3u) | (fld(1u, (dv >> 2) & 3u) << 9) | (fld(8u, (dv >> 4) & 3u) << 18));
         } else {
           const unsigned fH = (unsigned)(TB_FH >> (16 * (dv & 3u))) & 0x1ffu;

@@ -16,6 +16,8 @@ enum msa_alg {
   MSA_ALG_PART = 4,  // partial.cpp Gotoh with int32 wrap semantics
   MSA_ALG_SWL0 = 5,  // Smith-Waterman, linear gap, every substitution score >= 0 (plan's
                      // choice for MSA_SW_LINEAR when match, mismatch >= 0: no zero floor)
+  MSA_ALG_REF1 = 6,  // reference Gotoh, start type -1 (main_alignment_function's subproblem),
+                     // direction bytes: the tagged-max form of MSA_ALG_REF (msa_kernels.hip)
 };
 
 // Per-cell outputs.
