@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c2", choices=["c2", "c4", "c3", "c5", "ref"])
     ap.add_argument("--ref-len", type=int, default=10000, help="ref workload: seq0 x seq1 prefix length")
+    ap.add_argument("--pairs", type=int, default=0,
+                    help="c4: run only the first PAIRS of the 1024 pairs (e.g. 128 = one rank's share at N=8)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--synthetic", action="store_true", help="i.i.d. ACGT (splitmix seed) instead of the dataset")
     return ap.parse_args()
@@ -176,7 +178,7 @@ def main():
         desc = (f"main_alignment_function's path: reference Gotoh {m}x{n} (seq0 x seq1, g=1 h=2, start/end type -1), "
                 f"1 B/cell direction bytes + find_alignment's walk on the device")
     else:  # c4
-        total = data.C4_PAIRS
+        total = args.pairs if args.pairs > 0 else data.C4_PAIRS
         L = data.C4_LEN
         B = data.c4_reference(syn)
         from cse305_parallel_sequence_alignment_amd.shard import shard_range
@@ -307,7 +309,7 @@ def main():
         got = [int(x) for x in gathered.cpu().tolist()]
         fx = REPO / "tests" / "golden" / "c4_scores.json"
         if not syn and fx.exists():
-            checks["scores_match_fixture"] = got == json.loads(fx.read_text())["scores"]
+            checks["scores_match_fixture"] = got == json.loads(fx.read_text())["scores"][:total]
         checks["score_rank_block_matches_cpu_sample"] = all(
             got[lo + k] == O.sw(qs[k], B, 1, 0, 1, 1)["score"] for k in (0, len(qs) // 2, len(qs) - 1) if qs)
     ok = torch.tensor([int(all(checks.values()))], dtype=torch.int32, device=dev)
