@@ -212,7 +212,7 @@ StreamPool& stream_pool() {
 
 int nc_of(int alg) {
   switch (alg) {
-    case MSA_ALG_SWL: case MSA_ALG_SWL0: return 1;
+    case MSA_ALG_SWL: case MSA_ALG_SWL0: case MSA_ALG_SWLP: return 1;
     case MSA_ALG_SWA: case MSA_ALG_NWA: case MSA_ALG_REF1: return 2;
     default: return 3;
   }
@@ -268,6 +268,9 @@ kfn_t pick_kernel(int alg, int out, int tp, bool sgl) {
     case MSA_ALG_SWL:
       if (out == MSA_OUT_NONE) K3(MSA_ALG_SWL, MSA_OUT_NONE);
       if (out == MSA_OUT_H) K3(MSA_ALG_SWL, MSA_OUT_H);
+      break;
+    case MSA_ALG_SWLP:
+      if (out == MSA_OUT_NONE && !sgl && tp == 0) return kf<MSA_ALG_SWLP, MSA_OUT_NONE, 0>(false);
       break;
     case MSA_ALG_SWL0:
       if (out == MSA_OUT_NONE) K3(MSA_ALG_SWL0, MSA_OUT_NONE);
@@ -453,6 +456,21 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   switch (alg) {
     case MSA_SW_LINEAR:
       kalg = (desc->match >= 0 && desc->mismatch >= 0) ? MSA_ALG_SWL0 : MSA_ALG_SWL;
+      if (kalg == MSA_ALG_SWL0 && !desc->single && out_mode == MSA_OUT_NONE && !desc->track_end &&
+          desc->n_pairs >= 2) {
+        // score-only batch: two pairs per lane as packed int16 (MSA_ALG_SWLP) when every pair
+        // couple (2c, 2c+1) shares its row / column counts and column sequence (one stripe
+        // geometry, one code stream) and G = H + g(i+j) stays inside int16
+        bool pk = true;
+        const int64_t g = desc->gap_extend, smax = std::max({0, desc->match, desc->mismatch});
+        for (int64_t p = 0; p < desc->n_pairs && pk; ++p) {
+          const int64_t q = (p & 1) ? p - 1 : p;
+          pk = desc->m[p] == desc->m[q] && desc->n[p] == desc->n[q] && desc->b_off[p] == desc->b_off[q] &&
+               g * (desc->m[p] + desc->n[p] + 2) + smax * std::min(desc->m[p], desc->n[p]) + 2 * g + 127 < 32000 &&
+               desc->match + 2 * g <= 127;
+        }
+        if (pk) kalg = MSA_ALG_SWLP;
+      }
       break;
     case MSA_SW_AFFINE: kalg = MSA_ALG_SWA; break;
     case MSA_NW_BANDED: kalg = MSA_ALG_NWA; break;
@@ -516,7 +534,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   kp.mismatch = desc->mismatch;
   kp.gap_open = desc->gap_open;
   kp.gap_ext = desc->gap_extend;
-  if (kalg == MSA_ALG_SWL || kalg == MSA_ALG_SWL0) kp.gap_open = kp.gap_ext = desc->gap_extend;
+  if (kalg == MSA_ALG_SWL || kalg == MSA_ALG_SWL0 || kalg == MSA_ALG_SWLP) kp.gap_open = kp.gap_ext = desc->gap_extend;
   kp.h = desc->gap_open - desc->gap_extend;
   kp.start_type = desc->start_type;
   kp.band = band;
@@ -531,7 +549,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   for (int64_t p = 0; p < desc->n_pairs; ++p) {
     const int64_t m = desc->m[p], n = desc->n[p];
     if (m <= 0 || n <= 0 || m > (1 << 26) || n > (1 << 26)) { delete P; return MSA_ERR_ARG; }
-    if (kalg == MSA_ALG_SWL || kalg == MSA_ALG_SWL0) {
+    if (kalg == MSA_ALG_SWL || kalg == MSA_ALG_SWL0 || kalg == MSA_ALG_SWLP) {
       // shifted recurrence G = H + g*(i+j): G must stay far from the -2^30 sentinel
       // and from int32 overflow; the profile byte holds score + 2g
       const int64_t g = kp.gap_open;
@@ -604,7 +622,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     const int S = (int)((desc->m[0] + 64 * P->R - 1) / (64 * P->R));
     kp.n_items = (S + W - 1) / W;
   } else {
-    kp.n_items = (int)desc->n_pairs;
+    kp.n_items = (kalg == MSA_ALG_SWLP) ? (int)((desc->n_pairs + 1) / 2) : (int)desc->n_pairs;
   }
   const size_t lds_ints = 16 + (size_t)kp.sched_cap * 8 + (size_t)(2 * W + 1) * P->nc * MSA_RING +
                           (size_t)P->nc * kp.lds_row_words +
@@ -646,11 +664,15 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   // launch is one long chain of ~S x 8 phases.  Chunked mode runs it as n_chunks
   // independent chains of chunk_c (+ warm-up) stripes at once (rank convergence,
   // msa_kernels.hip header), with the exact launch kept behind it as the fallback.
+// Measured on MI355X for C3 (profiles/r03_c3_*): (warm, chunk) = (24, 24) 0.925 ms, (24, 12)
+// 0.768, (16, 16) 0.733, (20, 10) 0.678 -- and (16, 8) did not converge in every chunk (the
+// exact fallback ran: 18.3 ms).  C3's pair converges within ~900 rows, its synthetic mutated
+// copy within ~1,024; 20 stripes = 1,280 rows.
 #ifndef MSA_CHUNK_WARM
-#define MSA_CHUNK_WARM 24  // warm-up stripes (1,536 rows): C3's pair converges within ~900
+#define MSA_CHUNK_WARM 20  // warm-up stripes
 #endif
 #ifndef MSA_CHUNK_MIN
-#define MSA_CHUNK_MIN 24   // stripes per chunk, at least
+#define MSA_CHUNK_MIN 10   // stripes per chunk, at least
 #endif
   constexpr int kWarm = MSA_CHUNK_WARM;
   if (single && kalg == MSA_ALG_NWA && band >= 0 && (out_mode == MSA_OUT_H || out_mode == MSA_OUT_NONE)) {
@@ -820,7 +842,8 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
   a.nseg = P->nseg;
   a.nblk = P->nblk;
   {
-    const unsigned virt = (P->kp.alg == MSA_ALG_SWL || P->kp.alg == MSA_ALG_SWL0 || P->kp.alg == MSA_ALG_SWA) ? MSA_VIRT_CODE : 0u;
+    const unsigned virt = (P->kp.alg == MSA_ALG_SWL || P->kp.alg == MSA_ALG_SWL0 || P->kp.alg == MSA_ALG_SWLP ||
+                           P->kp.alg == MSA_ALG_SWA) ? MSA_VIRT_CODE : 0u;
     hipLaunchKernelGGL(stage_codes_kernel, dim3(64, (unsigned)P->segs.size()), dim3(256), 0, st, dB, P->d_segs,
                        (int)P->segs.size(), P->d_cod, (long long)P->cod_copy, virt, P->d_ticket);
     HIPCHK(hipGetLastError());
@@ -859,7 +882,8 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
     HIPCHK(hipGetLastError());
     return MSA_OK;
   }
-  const int sw = (P->kp.alg == MSA_ALG_SWL || P->kp.alg == MSA_ALG_SWL0 || P->kp.alg == MSA_ALG_SWA) ? 1 : 0;
+  const int sw = (P->kp.alg == MSA_ALG_SWL || P->kp.alg == MSA_ALG_SWL0 || P->kp.alg == MSA_ALG_SWLP ||
+                  P->kp.alg == MSA_ALG_SWA) ? 1 : 0;
   const int np = (int)P->d.n_pairs;
   hipLaunchKernelGGL(reduce_pairs_kernel, dim3(np), dim3(64), 0, st, P->d_pairs, P->d_meta, np, sw,
                      P->d_res);

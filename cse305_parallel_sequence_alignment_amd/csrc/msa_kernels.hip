@@ -77,14 +77,26 @@ namespace msa {
 template <int ALG> struct Tr;
 template <> struct Tr<MSA_ALG_SWL> { static constexpr int NC = 1; };
 template <> struct Tr<MSA_ALG_SWL0> { static constexpr int NC = 1; };
-// SW linear in shifted space (either kernel id)
-constexpr bool swlin(int alg) { return alg == MSA_ALG_SWL || alg == MSA_ALG_SWL0; }
+template <> struct Tr<MSA_ALG_SWLP> { static constexpr int NC = 1; };
+// SW linear in shifted space (any of the three kernel ids)
+constexpr bool swlin(int alg) { return alg == MSA_ALG_SWL || alg == MSA_ALG_SWL0 || alg == MSA_ALG_SWLP; }
+// two pairs per lane: every carried value is two int16 (pair 2c low, pair 2c+1 high)
+constexpr bool pk16(int alg) { return alg == MSA_ALG_SWLP; }
 template <> struct Tr<MSA_ALG_SWA> { static constexpr int NC = 2; };
 template <> struct Tr<MSA_ALG_NWA> { static constexpr int NC = 2; };
 template <> struct Tr<MSA_ALG_REF> { static constexpr int NC = 3; };
 template <> struct Tr<MSA_ALG_REF1> { static constexpr int NC = 2; };
 template <> struct Tr<MSA_ALG_PART> { static constexpr int NC = 3; };
 
+// packed int16 helpers (v_pk_add_u16 / v_pk_max_i16 on gfx950)
+typedef short msa_s2 __attribute__((ext_vector_type(2)));
+__host__ __device__ __forceinline__ int pk2(int v) { return (int)(((unsigned)v & 0xffffu) * 0x10001u); }
+__device__ __forceinline__ int pk_add(int a, int b) {
+  return __builtin_bit_cast(int, __builtin_bit_cast(msa_s2, a) + __builtin_bit_cast(msa_s2, b));
+}
+__device__ __forceinline__ int pk_max(int a, int b) {
+  return __builtin_bit_cast(int, __builtin_elementwise_max(__builtin_bit_cast(msa_s2, a), __builtin_bit_cast(msa_s2, b)));
+}
 __device__ __forceinline__ int dpp_shr1(int old, int src) {
   return __builtin_amdgcn_update_dpp(old, src, 0x138, 0xf, 0xf, false);
 }
@@ -172,7 +184,8 @@ __device__ __forceinline__ void border_top(const msa_kparams& kp, int c, int (&v
   // row-0 border's tent moved to the diagonal, H = -h - g*|c - r0| inside the band.
   if constexpr (swlin(ALG)) {
     // G(0,c) = H(0,c) + g*c = g*c; SWL0 also on the virtual columns c < 0
-    v[0] = (c >= 0 || ALG == MSA_ALG_SWL0) ? kp.gap_open * c : MSA_NEG;
+    v[0] = (c >= 0 || ALG == MSA_ALG_SWL0 || ALG == MSA_ALG_SWLP) ? kp.gap_open * c : MSA_NEG;
+    if constexpr (pk16(ALG)) v[0] = pk2(v[0]);
     v[1] = MSA_NEG;
     v[2] = MSA_NEG;
   } else if constexpr (ALG == MSA_ALG_SWA) {
@@ -230,7 +243,7 @@ template <int ALG>
 __device__ __forceinline__ void border_left(const msa_kparams& kp, int i, int (&v)[3]) {
   // Column 0 of row i (i >= 1), state order of each algorithm.
   if constexpr (swlin(ALG)) {
-    v[0] = kp.gap_open * i;  // G(i,0) = H(i,0) + g*i
+    v[0] = pk16(ALG) ? pk2(kp.gap_open * i) : kp.gap_open * i;  // G(i,0) = H(i,0) + g*i
     v[1] = MSA_NEG;
     v[2] = MSA_NEG;
   } else if constexpr (ALG == MSA_ALG_SWA) {
@@ -266,6 +279,7 @@ __device__ __forceinline__ void border_left(const msa_kparams& kp, int i, int (&
 template <int ALG>
 struct LaneState {
   int S[3];    // left-cell state (algorithm order, see step())
+  unsigned plo2, phi2;  // SWLP: the second pair's profile
   int U[3];    // diagonal values (previous step's up values)
   int LB[3];   // left border held while t < tmin
   int tmin, tmax;
@@ -300,6 +314,12 @@ __device__ __forceinline__ unsigned step(const msa_kparams& kp, LaneState<ALG>& 
     nS[0] = imax3(x, up, L.S[0]);
     // opaque: keeps G a real per-step value (otherwise LLVM flattens the
     // running max3 chain and distributes the "- ct" over every term)
+    asm("" : "+v"(nS[0]));
+    L.U[0] = up;
+  } else if constexpr (ALG == MSA_ALG_SWLP) {
+    // MSA_ALG_SWL0 on two pairs at once: s holds both pairs' score + 2g as int16
+    const int up = dpp_shr1(in[0], L.S[0]);
+    nS[0] = pk_max(pk_max(pk_add(L.U[0], s), up), L.S[0]);
     asm("" : "+v"(nS[0]));
     L.U[0] = up;
   } else if constexpr (ALG == MSA_ALG_SWL0) {
@@ -425,7 +445,12 @@ __device__ __forceinline__ unsigned step(const msa_kparams& kp, LaneState<ALG>& 
       }
     }
   } else {
-    if constexpr (swlin(ALG) || ALG == MSA_ALG_SWA) {
+    if constexpr (pk16(ALG)) {
+      static_assert(TRACKPOS == 0, "packed pairs: score only");
+      const int hv = pk_add(nS[0], pk2(-ct));  // both pairs' H = G - g(i+j)
+      hout = hv;
+      L.best = pk_max(L.best, hv);
+    } else if constexpr (swlin(ALG) || ALG == MSA_ALG_SWA) {
       const int hv = swlin(ALG) ? nS[0] - ct : nS[0];
       hout = hv;
       if constexpr (TRACKPOS == 2) {
@@ -638,12 +663,14 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
       ns = ke - kb;
       nwarm = ks0 - kb;
     } else {
-      pair = item;
+      pair = pk16(ALG) ? 2 * item : item;  // SWLP: item c = pairs 2c (low halves) and 2c+1 (high)
       group = 0;
       k0 = 0;
-      ns = (a.pairs[item].m + 63) / 64;
+      ns = (a.pairs[pair].m + 63) / 64;
     }
     const msa_pair_desc pd = a.pairs[pair];
+    // SWLP: the pair in the high halves (the last item of an odd count repeats its low pair)
+    const msa_pair_desc pd2 = pk16(ALG) ? a.pairs[min(pair + 1, kp.n_pairs - 1)] : pd;
     const int m = pd.m, n = pd.n;
     const int S_pair = (m + 63) / 64;
 
@@ -891,6 +918,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
       const int ks = k0 + cur;  // pair-local stripe index
       const int row_i = 64 * ks + lane + 1;
       const unsigned ac = (row_i <= m) ? (a.A[pd.a_off + row_i - 1] & 7u) : 0u;
+      const unsigned ac2 = (pk16(ALG) && row_i <= m) ? (a.A[pd2.a_off + row_i - 1] & 7u) : 0u;
       for (; ph < sg.T; ++ph) MSA_SYNC(ph);
       // ---- stripe init ----
       LaneState<ALG> L;
@@ -913,6 +941,10 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
       if constexpr (swlin(ALG)) {
         L.S[0] = gdiag - kp.gap_open;      // G(i, cs-r-1)
         L.U[0] = gdiag - 2 * kp.gap_open;  // G(i-1, cs-r-1)
+        if constexpr (pk16(ALG)) {
+          L.S[0] = pk2(L.S[0]);
+          L.U[0] = pk2(L.U[0]);
+        }
       }
       // substitution profile of this row (codes 0..7)
       {
@@ -923,17 +955,23 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
         else if constexpr (swlin(ALG)) { sm = kp.match + 2 * kp.gap_open; sx = kp.mismatch + 2 * kp.gap_open; }
         else { sm = kp.match; sx = kp.mismatch; }
         const unsigned bx = (unsigned)(sx & 0xff) * 0x01010101u;
-        unsigned lo = bx, hi = bx;
-        const unsigned bm = (unsigned)(sm & 0xff);
-        if (ac < 4) lo = (lo & ~(0xffu << (8 * ac))) | (bm << (8 * ac));
-        else hi = (hi & ~(0xffu << (8 * (ac - 4)))) | (bm << (8 * (ac - 4)));
-        // virtual columns: SWL0 scores them 0, so (floor-free) G = g*(i+j), i.e.
-        // H = 0, holds exactly on every cell left of column 1 -- the border
-        // column itself; right of column n they never beat a real cell
-        if constexpr (ALG == MSA_ALG_SWL0) hi = (hi & 0x00ffffffu) | ((unsigned)((2 * kp.gap_open) & 0xff) << 24);
-        else if constexpr (SWK) hi = (hi & 0x00ffffffu) | ((unsigned)(MSA_VIRT_SCORE & 0xff) << 24);
-        L.plo = lo;
-        L.phi = hi;
+        auto table = [&](unsigned c, unsigned& plo_, unsigned& phi_) __attribute__((always_inline)) {
+          unsigned lo = bx, hi = bx;
+          const unsigned bm = (unsigned)(sm & 0xff);
+          if (c < 4) lo = (lo & ~(0xffu << (8 * c))) | (bm << (8 * c));
+          else hi = (hi & ~(0xffu << (8 * (c - 4)))) | (bm << (8 * (c - 4)));
+          // virtual columns: SWL0 scores them 0, so (floor-free) G = g*(i+j), i.e.
+          // H = 0, holds exactly on every cell left of column 1 -- the border
+          // column itself; right of column n they never beat a real cell
+          if constexpr (ALG == MSA_ALG_SWL0 || ALG == MSA_ALG_SWLP)
+            hi = (hi & 0x00ffffffu) | ((unsigned)((2 * kp.gap_open) & 0xff) << 24);
+          else if constexpr (SWK) hi = (hi & 0x00ffffffu) | ((unsigned)(MSA_VIRT_SCORE & 0xff) << 24);
+          plo_ = lo;
+          phi_ = hi;
+        };
+        table(ac, L.plo, L.phi);
+        L.plo2 = L.phi2 = 0;
+        if constexpr (pk16(ALG)) table(ac2, L.plo2, L.phi2);
       }
       // code stream: lane r needs columns cs - r + t; column c sits in copy
       // (c-1+CPAD)&15 at byte (c-1+CPAD) & ~15, so every read is an aligned dwordx4
@@ -1042,7 +1080,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
               for (int k = 0; k < KS; ++k) {
                 const bool o = sg.cs + KS * q + k > out_chi;
 #pragma unroll
-                for (int v = 0; v < NC; ++v) IN[v][k] = o ? MSA_NEG : IN[v][k];
+                for (int v = 0; v < NC; ++v) IN[v][k] = o ? (pk16(ALG) ? (int)0x80008000u : MSA_NEG) : IN[v][k];
               }
             }
           }
@@ -1079,12 +1117,15 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
 #pragma unroll
         for (int u = 0; u < KS / 4; ++u) {
           const unsigned s4 = __builtin_amdgcn_perm(L.phi, L.plo, cw[u]);
+          const unsigned s4b = pk16(ALG) ? __builtin_amdgcn_perm(L.phi2, L.plo2, cw[u]) : 0u;
           unsigned dq = 0;
 #pragma unroll
           for (int kk = 0; kk < 4; ++kk) {
             const int k = 4 * u + kk;
             const int t = KS * q + k;
-            const int s = ((int)(s4 << (24 - 8 * kk))) >> 24;
+            // SWLP: {s4 byte kk, 0, s4b byte kk, 0} = both pairs' score + 2g as int16 (>= 0)
+            const int s = pk16(ALG) ? (int)__builtin_amdgcn_perm(s4b, s4, 0x0c000c00u | ((4u + kk) << 16) | (unsigned)kk)
+                                    : ((int)(s4 << (24 - 8 * kk))) >> 24;
             int inv[3];
 #pragma unroll
             for (int v = 0; v < NC; ++v) inv[v] = IN[v][k];
@@ -1279,7 +1320,30 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
       // ---- stripe finalize ----
       msa_stripe_meta* md = a.meta + pd.stripe0 + ks;
       if (!outp) continue;  // a warm-up stripe: its meta belongs to the chunk that outputs it
-      if constexpr (swlin(ALG) || ALG == MSA_ALG_SWA) {
+      if constexpr (pk16(ALG)) {
+        // each half separately: pair 2c's best (low halves), then pair 2c+1's (high halves)
+        msa_stripe_meta* md2 = a.meta + pd2.stripe0 + ks;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const int bv = half ? (L.best >> 16) : (int)(short)(L.best & 0xffff);
+          int b = (L.i <= m) ? bv : INT32_MIN;
+          int bi = L.i;
+#pragma unroll
+          for (int off = 32; off >= 1; off >>= 1) {
+            const int ob = __shfl_xor(b, off);
+            const int oi = __shfl_xor(bi, off);
+            if (ob > b || (ob == b && oi < bi)) { b = ob; bi = oi; }
+          }
+          if (lane == 0) {
+            msa_stripe_meta* mh = half ? md2 : md;
+            mh->best = b;
+            mh->best_i = bi;
+            mh->best_j = -1;
+            mh->cs = sg.cs;
+            mh->phases = sg.P * CPP;
+          }
+        }
+      } else if constexpr (swlin(ALG) || ALG == MSA_ALG_SWA) {
         // first max in row-major order: max best, then min row
         const int bv = (TRACKPOS == 2) ? (L.best >> 15) : L.best;
         const int bt = (TRACKPOS == 2) ? 32767 - (L.best & 32767) : L.bt;
@@ -1431,11 +1495,17 @@ __global__ __launch_bounds__(256) void chunk_add_kernel(int32_t* H, const msa_pa
   if (!sh_ok || e == 0 || H == nullptr) return;
   const int ks0 = k * chunk_c, ke = min(S, ks0 + chunk_c);
   const size_t per = (size_t)pd.pmax * MSA_K * 64;  // int32 cells per stripe
-  int4* p = reinterpret_cast<int4*>(H + pd.out_off + (size_t)ks0 * per);
-  const size_t nv = (size_t)(ke - ks0) * per / 4;
-  for (size_t x = (size_t)blockIdx.x * 256 + threadIdx.x; x < nv; x += (size_t)gridDim.x * 256) {
-    const msa_v4i v = __builtin_nontemporal_load(reinterpret_cast<const msa_v4i*>(p + x));
-    __builtin_nontemporal_store(msa_v4i{v.x + e, v.y + e, v.z + e, v.w + e}, reinterpret_cast<msa_v4i*>(p + x));
+  msa_v4i* p = reinterpret_cast<msa_v4i*>(H + pd.out_off + (size_t)ks0 * per);
+  const size_t nv = (size_t)(ke - ks0) * per / 4;  // per is a multiple of 1024: nv of 256
+  const size_t step = (size_t)gridDim.x * 1024;
+  for (size_t x0 = (size_t)blockIdx.x * 1024 + threadIdx.x; x0 < nv; x0 += step) {  // 4 loads in flight
+    msa_v4i v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (x0 + 256 * u < nv) v[u] = __builtin_nontemporal_load(p + x0 + 256 * u);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (x0 + 256 * u < nv) __builtin_nontemporal_store(v[u] + e, p + x0 + 256 * u);
   }
 }
 

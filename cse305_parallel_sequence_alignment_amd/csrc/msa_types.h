@@ -18,6 +18,8 @@ enum msa_alg {
                      // choice for MSA_SW_LINEAR when match, mismatch >= 0: no zero floor)
   MSA_ALG_REF1 = 6,  // reference Gotoh, start type -1 (main_alignment_function's subproblem),
                      // direction bytes: the tagged-max form of MSA_ALG_REF (msa_kernels.hip)
+  MSA_ALG_SWLP = 7,  // MSA_ALG_SWL0 for TWO pairs per lane as packed int16 (batch, score only:
+                     // pairs 2c and 2c+1 share rows/columns counts and the column sequence)
 };
 
 // Per-cell outputs.
