@@ -176,6 +176,38 @@ def test_sw_linear_c4_shape_scores(oracle, dev, LB):
         assert res[k]["score"] == oracle.sw(As[k], B, 1, 0, 1, 1)["score"]
 
 
+@pytest.mark.parametrize("scoring", [(1, 0, 1), (2, 1, 1), (3, 0, 2), (5, 2, 3)])
+def test_sw_linear_packed_pairs(oracle, dev, LB, scoring):
+    """Score-only batches whose pair couples (2c, 2c+1) share sizes and column sequence run two pairs per lane
+    as packed int16 (MSA_ALG_SWLP): every score equals the oracle's -- couples of different shapes in one plan,
+    an odd pair count (the last couple repeats its pair), similar and random pairs, sizes from 1 to 2,000."""
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+
+    ma, mi, g = scoring
+    rng = np.random.default_rng(40 + ma)
+    shapes = [(700, 650), (700, 650), (64, 64), (64, 64), (1, 9), (1, 9), (2000, 1999), (2000, 1999), (130, 7),
+              (130, 7), (333, 1000)]
+    Bs = {}
+    As, ao, bo, Bcat = [], [], [], b""
+    for k, (m, n) in enumerate(shapes):
+        c = k // 2
+        if c not in Bs:
+            Bs[c] = (len(Bcat), rs(rng, n))
+            Bcat += Bs[c][1]
+        B = Bs[c][1]
+        A = B[:m] if (k % 4 == 1 and m <= n) else rs(rng, m)  # some similar pairs (long runs of matches)
+        ao.append(sum(len(x) for x in As))
+        As.append(A)
+        bo.append(Bs[c][0])
+    pl = Plan(LB.SW_LINEAR, LB.CELLS_NONE, [m for m, _ in shapes], [n for _, n in shapes], ao, bo, match=ma,
+              mismatch=mi, gap_open=g, gap_extend=g, single=False)
+    pl.run(_dev(b"".join(As), dev), _dev(Bcat, dev))
+    res = pl.results()
+    for k, (m, n) in enumerate(shapes):
+        B = Bs[k // 2][1]
+        assert res[k]["score"] == oracle.sw(As[k], B, ma, mi, g, g)["score"], (k, m, n)
+
+
 def test_main_alignment_kat_and_harness(oracle, dev, dataset):
     """main_alignment_function stdout (main_alignment.cpp:353-410) byte-exact on the KAT and harness pairs."""
     from cse305_parallel_sequence_alignment_amd import api
