@@ -506,7 +506,8 @@ def test_c3_full_size(oracle, dev, LB):
     assert pl.results()[0]["score"] == int(score)
     assert pl.checksum(H) == digest
     # the bench's pair converges in every chunk: the cells come from the chunked launch
-    assert pl.run_info() == dict(mode="chunked", chunks=pl.run_info()["chunks"], converged=1, warm_stripes=24)
+    info = pl.run_info()
+    assert info["mode"] == "chunked" and info["converged"] == 1 and info["chunks"] >= 4, info
 
 
 def _similar(rng, m, sub=0.02, indel=0.002):
