@@ -623,6 +623,20 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     kp.n_items = (S + W - 1) / W;
   } else {
     kp.n_items = (kalg == MSA_ALG_SWLP) ? (int)((desc->n_pairs + 1) / 2) : (int)desc->n_pairs;
+    // A batch with fewer pairs (couples) than two workgroups per CU leaves CUs idle while each
+    // workgroup walks its pair's whole stripe chain (C4 at 8 GPUs: 128 pairs per rank).  Then
+    // every pair is split into groups of W stripes, one item each, chained through granules
+    // (kp.single == 3): a pair's stripes run on several CUs at once.
+    bool eq_m = true;
+    for (int64_t p = 1; p < desc->n_pairs; ++p) eq_m = eq_m && desc->m[p] == desc->m[0];
+    const int S0 = (int)((desc->m[0] + 63) / 64);
+    if (eq_m && kp.n_items < 2 * device_cus() && S0 >= 2 * W && band < 0) {
+      kp.single = 3;
+      kp.groups = (S0 + W - 1) / W;
+      kp.n_items *= kp.groups;
+      kp.sched_cap = W;
+      kp.lds_row_words = 0;  // no wrap link: an item holds at most W stripes
+    }
   }
   const size_t lds_ints = 16 + (size_t)kp.sched_cap * 8 + (size_t)(2 * W + 1) * P->nc * MSA_RING +
                           (size_t)P->nc * kp.lds_row_words +
@@ -729,9 +743,13 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   if (!P->alloc(&P->d_res, sizeof(PairResult) * desc->n_pairs)) return fail();
   if (!P->alloc(&P->d_sum, 64)) return fail();
   const int single_items = P->chunked ? P->fb_kp.n_items : kp.n_items;  // single-mode launch's items
-  if (single && single_items > 1) {
-    P->gbuf_stride = (int)(((desc->n[0] + 2 * MSA_GOFF + 16) + 15) & ~15);
-    const size_t gb = (size_t)(single_items - 1) * P->nc * P->gbuf_stride * sizeof(unsigned long long);
+  if ((single || kp.single == 3) && single_items > 1) {
+    int64_t nmax = 0;
+    for (int64_t p = 0; p < desc->n_pairs; ++p) nmax = std::max(nmax, desc->n[p]);
+    P->gbuf_stride = (int)(((nmax + 2 * MSA_GOFF + 16) + 15) & ~15);
+    // (mode 3: item k publishes into slot k, so one slot per item)
+    const size_t gb = (size_t)(kp.single == 3 ? single_items : single_items - 1) * P->nc * P->gbuf_stride *
+                      sizeof(unsigned long long);
     if (!P->alloc(&P->d_gbuf, gb)) return fail();
     if (hipMemset(P->d_gbuf, 0, gb) != hipSuccess) return fail();
   }

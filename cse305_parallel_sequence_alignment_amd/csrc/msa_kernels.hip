@@ -649,6 +649,15 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
       const msa_pair_desc pd0 = a.pairs[0];
       const int S = (pd0.m + 63) / 64;
       ns = min(W, S - k0);
+    } else if (kp.single == 3) {
+      // a batch of equal-m pairs too small to fill the chip: every pair (SWLP: couple) is split
+      // into kp.groups items of W stripes, consecutive tickets, chained through granules
+      const int pidx = item / kp.groups;
+      group = item - pidx * kp.groups;
+      pair = pk16(ALG) ? 2 * pidx : pidx;
+      k0 = group * W;
+      const int S = (a.pairs[pair].m + 63) / 64;
+      ns = min(W, S - k0);
     } else if (kp.single == 2) {
       pair = 0;
       group = item;
@@ -790,7 +799,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
 
     if (w == W) {
       // =================== loader wave ===================
-      const bool act = kp.single == 1 && group > 0;
+      const bool act = (kp.single == 1 || kp.single == 3) && group > 0;
       StripeGeom s0 = sched[0];
       s0.cs = uni(s0.cs);
       s0.P = uni(s0.P);
@@ -800,7 +809,8 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
         stripe_geom(k0 - 1, m, n, kp.band, gp, KS);
         chi = gp.c_hi;
       }
-      const unsigned long long* g_in = act ? a.gbuf + (size_t)(group - 1) * NC * a.gbuf_stride : a.gbuf;
+      // (single: item == group; mode 3: a pair's groups are consecutive items)
+      const unsigned long long* g_in = act ? a.gbuf + (size_t)(item - 1) * NC * a.gbuf_stride : a.gbuf;
       // the item holds the pair's first stripe: stage the DP's row 0; chunked: the guessed
       // row above the chunk's first (warm-up) stripe
       const bool border = (k0 == 0) || kp.single == 2;
@@ -820,7 +830,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
       // one phase later (after the barrier that completes them).
       const int sl_idx = ns - 1;
       // (with the DPP shift register the compute wave publishes itself)
-      const bool sink = kp.single == 1 && (k0 + sl_idx) < S_pair - 1 && !(NC == 1 && SGL);
+      const bool sink = (kp.single == 1 || kp.single == 3) && (k0 + sl_idx) < S_pair - 1 && !(NC == 1 && SGL);
       StripeGeom sl = sched[sl_idx];
       sl.T = uni(sl.T); sl.P = uni(sl.P); sl.cs = uni(sl.cs);
       int sl_out_cs = 0;
@@ -830,7 +840,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
         sl_out_cs = uni(gn.cs);
       }
       const int* ring_last = rings + ((((sl_idx / W) & 1) * W + sl_idx % W) * NC) * MSA_RING;
-      unsigned long long* g_out = a.gbuf + (size_t)group * NC * a.gbuf_stride;
+      unsigned long long* g_out = a.gbuf + (size_t)item * NC * a.gbuf_stride;
       auto sink_phase = [&](int q) __attribute__((always_inline)) {
         if (!sink || q < 0 || q >= sl.P) return;
         const int v = lane >> 4, l = lane & 15;
@@ -1014,7 +1024,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
         in_ptr = rings + ((par_in * W + (w - 1)) * NC) * MSA_RING; in_vs = MSA_RING; in_mask = MSA_RING - 1;
       }
       int snk;
-      if (cur == ns - 1) snk = (kp.single == 1 && ks < S_pair - 1) ? SNK_GLOBAL : SNK_NONE;
+      if (cur == ns - 1) snk = ((kp.single == 1 || kp.single == 3) && ks < S_pair - 1) ? SNK_GLOBAL : SNK_NONE;
       else snk = (cur % W == W - 1) ? SNK_ROW : SNK_RING;
       int* const ring_out = rings + (((cur / W) & 1) * W + w) * NC * MSA_RING;
       int* out_ptr;
@@ -1038,7 +1048,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
         out_chi = gp.c_hi;
       }
       snk = uni(snk); out_cs = uni(out_cs); out_chi = uni(out_chi);
-      unsigned long long* const g_out = a.gbuf + (size_t)group * NC * a.gbuf_stride;
+      unsigned long long* const g_out = a.gbuf + (size_t)item * NC * a.gbuf_stride;
       const size_t obase = (size_t)pd.out_off + (size_t)ks * pd.pmax * MSA_K * 64;  // pmax: 16-step blocks
       // chunked mode: warm-up stripes store no cells and no meta (another chunk owns them);
       // the warm-up's last stripe and the chunk's last stripe save lane 63's (H, F) row

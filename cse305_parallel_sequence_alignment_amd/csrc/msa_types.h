@@ -74,6 +74,9 @@ typedef struct msa_kparams {
   int32_t lds_row_words;    // wrap row buffer entries per carried value (batch mode)
   int32_t chunk_c;          // single == 2: stripes each chunk outputs
   int32_t chunk_warm;       // single == 2: warm-up stripes computed before a chunk's first one
+  int32_t groups;           // single == 3 (a batch too small to fill the chip): items per pair (or
+                            //   per packed couple), each W consecutive stripes, chained through
+                            //   granules like single mode; every pair has the same m
 } msa_kparams;
 
 #ifdef __cplusplus

@@ -208,6 +208,57 @@ def test_sw_linear_packed_pairs(oracle, dev, LB, scoring):
         assert res[k]["score"] == oracle.sw(As[k], B, ma, mi, g, g)["score"], (k, m, n)
 
 
+@pytest.mark.parametrize("kind", ["packed", "int32_H", "affine_dir"])
+def test_batch_split_pairs(oracle, dev, LB, kind):
+    """A batch with fewer pairs than two workgroups per CU splits every pair into items of W stripes chained
+    through granules (kp.single == 3, the per-rank share of C4 at 8 GPUs): scores (and for the int32 plan the
+    full H matrices, for SW affine the device traceback) equal the oracle's."""
+    import torch
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+
+    rng = np.random.default_rng({"packed": 1, "int32_H": 2, "affine_dir": 3}[kind])
+    if kind == "packed":
+        K, m, n = 37, 1500, 1400  # odd count: the last couple repeats its pair
+        As = [rs(rng, m) for _ in range(K)]
+        B = rs(rng, n)
+        pl = Plan(LB.SW_LINEAR, LB.CELLS_NONE, [m] * K, [n] * K, [k * m for k in range(K)], [0] * K, match=1,
+                  mismatch=0, gap_open=1, gap_extend=1, single=False)
+        pl.run(_dev(b"".join(As), dev), _dev(B, dev))
+        res = pl.results()
+        for k in range(K):
+            assert res[k]["score"] == oracle.sw(As[k], B, 1, 0, 1, 1)["score"], k
+    elif kind == "int32_H":
+        K, m = 6, 1100
+        ns = [900, 1300, 1100, 700, 1250, 1000]
+        As = [rs(rng, m) for _ in range(K)]
+        Bs = [rs(rng, x) for x in ns]
+        bo = np.cumsum([0] + ns)[:-1]
+        pl = Plan(LB.SW_LINEAR, LB.CELLS_H, [m] * K, ns, [k * m for k in range(K)], bo, match=2, mismatch=-1,
+                  gap_open=1, gap_extend=1, track_end=True, single=False)
+        H = torch.empty(pl.cells_elems, dtype=torch.int32, device=dev)
+        pl.run(_dev(b"".join(As), dev), _dev(b"".join(Bs), dev), H)
+        res, meta, Hh = pl.results(), pl.stripe_meta(), H.cpu().numpy()
+        for k in range(K):
+            o = oracle.sw(As[k], Bs[k], 2, -1, 1, 1, want_h=True)
+            assert res[k]["score"] == o["score"] and tuple(res[k]["end"]) == tuple(o["end"]), k
+            assert np.array_equal(pl.deskew(Hh, k, meta)[1:, 1:], o["H"][1:, 1:]), k
+    else:
+        K, m, n = 5, 1300, 1250
+        As = [rs(rng, m) for _ in range(K)]
+        Bs = [rs(rng, n) for _ in range(K)]
+        pl = Plan(LB.SW_AFFINE, LB.CELLS_DIR, [m] * K, [n] * K, [k * m for k in range(K)], [k * n for k in range(K)],
+                  match=1, mismatch=0, gap_open=3, gap_extend=1, track_end=True, single=False)
+        D = torch.empty(pl.cells_elems, dtype=torch.uint8, device=dev)
+        pl.run(_dev(b"".join(As), dev), _dev(b"".join(Bs), dev), D)
+        res = pl.results()
+        for k in range(K):
+            o = oracle.sw(As[k], Bs[k], 1, 0, 3, 1, want_tb=True)
+            tb = pl.traceback(D, pair=k)
+            assert (res[k]["score"], tuple(res[k]["end"])) == (o["score"], tuple(o["end"])), k
+            assert (tuple(tb["beg"]), tb["cigar"]) == (tuple(o["beg"]), o["cigar"]), k
+    assert pl.error() == 0
+
+
 def test_main_alignment_kat_and_harness(oracle, dev, dataset):
     """main_alignment_function stdout (main_alignment.cpp:353-410) byte-exact on the KAT and harness pairs."""
     from cse305_parallel_sequence_alignment_amd import api
