@@ -625,17 +625,27 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     kp.n_items = (kalg == MSA_ALG_SWLP) ? (int)((desc->n_pairs + 1) / 2) : (int)desc->n_pairs;
     // A batch with fewer pairs (couples) than two workgroups per CU leaves CUs idle while each
     // workgroup walks its pair's whole stripe chain (C4 at 8 GPUs: 128 pairs per rank).  Then
-    // every pair is split into groups of W stripes, one item each, chained through granules
-    // (kp.single == 3): a pair's stripes run on several CUs at once.
+    // every pair is split into items of C stripes (a multiple of W; C sized so that the items
+    // about fill two workgroups per CU), chained through granules (kp.single == 3): a pair's
+    // stripes run on several CUs at once.  Measured (C4 shape, 4k x 4k, packed couples):
+    // C = W = 8 for 64 couples 1.72 -> 0.81 ms; C = W for 256 couples was slower than one
+    // item per couple would be (2.38 ms), hence C grows with the couple count.
     bool eq_m = true;
     for (int64_t p = 1; p < desc->n_pairs; ++p) eq_m = eq_m && desc->m[p] == desc->m[0];
     const int S0 = (int)((desc->m[0] + 63) / 64);
-    if (eq_m && kp.n_items < 2 * device_cus() && S0 >= 2 * W && band < 0) {
-      kp.single = 3;
-      kp.groups = (S0 + W - 1) / W;
-      kp.n_items *= kp.groups;
-      kp.sched_cap = W;
-      kp.lds_row_words = 0;  // no wrap link: an item holds at most W stripes
+    const int slots = 2 * device_cus();
+    if (eq_m && kp.n_items < slots && S0 >= 2 * W && band < 0) {
+      int C = (int)(((int64_t)S0 * kp.n_items + slots - 1) / slots);
+      C = std::max(W, (C + W - 1) / W * W);
+      if (C < S0) {
+        kp.single = 3;
+        kp.chunk_c = C;
+        kp.groups = (S0 + C - 1) / C;
+        kp.n_items *= kp.groups;
+        kp.sched_cap = C;
+        // the wave W-1 -> wave 0 wrap link inside an item goes through the LDS row buffer
+        if (C <= W) kp.lds_row_words = 0;
+      }
     }
   }
   const size_t lds_ints = 16 + (size_t)kp.sched_cap * 8 + (size_t)(2 * W + 1) * P->nc * MSA_RING +

@@ -651,13 +651,14 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
       ns = min(W, S - k0);
     } else if (kp.single == 3) {
       // a batch of equal-m pairs too small to fill the chip: every pair (SWLP: couple) is split
-      // into kp.groups items of W stripes, consecutive tickets, chained through granules
+      // into kp.groups items of kp.chunk_c stripes (a multiple of W), consecutive tickets,
+      // chained through granules; inside an item the waves cycle as in batch mode
       const int pidx = item / kp.groups;
       group = item - pidx * kp.groups;
       pair = pk16(ALG) ? 2 * pidx : pidx;
-      k0 = group * W;
+      k0 = group * kp.chunk_c;
       const int S = (a.pairs[pair].m + 63) / 64;
-      ns = min(W, S - k0);
+      ns = min(kp.chunk_c, S - k0);
     } else if (kp.single == 2) {
       pair = 0;
       group = item;
