@@ -625,19 +625,20 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     kp.n_items = (kalg == MSA_ALG_SWLP) ? (int)((desc->n_pairs + 1) / 2) : (int)desc->n_pairs;
     // A batch with fewer pairs (couples) than two workgroups per CU leaves CUs idle while each
     // workgroup walks its pair's whole stripe chain (C4 at 8 GPUs: 128 pairs per rank).  Then
-    // every pair is split into items of C stripes (a multiple of W; C sized so that the items
-    // about fill two workgroups per CU), chained through granules (kp.single == 3): a pair's
-    // stripes run on several CUs at once.  Measured (C4 shape, 4k x 4k, packed couples):
-    // C = W = 8 for 64 couples 1.72 -> 0.81 ms; C = W for 256 couples was slower than one
-    // item per couple would be (2.38 ms), hence C grows with the couple count.
+    // every pair is split into items of W stripes, chained through granules (kp.single == 3):
+    // a pair's stripes run on several CUs at once.  Measured (C4 shape, 4k x 4k, packed
+    // couples, ms): 64 couples 1.72 -> 0.80, 128: 1.39, 256: 2.38.  Items of C > W stripes
+    // (fewer items, the waves cycling inside one) were slower at every count -- 128 couples
+    // with C = 16: 1.81, 256 with C = 32: 2.46 -- since an item's second round of stripes waits
+    // for its first to finish, so a pair's chain grows to ~(S / W) stripe lengths; kp.chunk_c
+    // stays general (the kernel runs any multiple of W) but the plan uses C = W.
     bool eq_m = true;
     for (int64_t p = 1; p < desc->n_pairs; ++p) eq_m = eq_m && desc->m[p] == desc->m[0];
     const int S0 = (int)((desc->m[0] + 63) / 64);
     const int slots = 2 * device_cus();
     if (eq_m && kp.n_items < slots && S0 >= 2 * W && band < 0) {
-      int C = (int)(((int64_t)S0 * kp.n_items + slots - 1) / slots);
-      C = std::max(W, (C + W - 1) / W * W);
-      if (C < S0) {
+      const int C = W;
+      {
         kp.single = 3;
         kp.chunk_c = C;
         kp.groups = (S0 + C - 1) / C;
