@@ -90,15 +90,48 @@ __device__ __forceinline__ int ref_end_state(const int32_t (&fin)[3], int end_ty
   return 2;
 }
 
-// REF = false: Smith-Waterman affine walk; true: the reference's Gotoh walk (end_type,
-// h: find_alignment's end rule).
-template <bool REF>
+// Walk kinds: Smith-Waterman affine; the reference's Gotoh walk over table numbers (REF
+// fill) or over tags (REF1 fill, tag = 4 - table).
+enum { TB_SW = 0, TB_REF = 1, TB_REF_TAG = 2 };
+
+// The transition word of a cell (see the window comment in traceback_kernel): three 9-bit
+// fields, field s = the lane step of leaving state s | 9 x the next state << 4 (27 = stop),
+// and bit 31 set.  With bit 31 set and 13 as the high word of the 64-bit shift in a step, the
+// stop state is absorbing: shifting by 27 yields lane step 0 and next state 27 again, so the
+// steps after a stop are no-ops and a window needs no branch per step.
+template <int KIND>
+__device__ __forceinline__ unsigned tb_word(unsigned dv) {
+  if constexpr (KIND == TB_REF_TAG) {
+    // table s leaves by its fixed move (T1 diagonal 9, T2 left 1, T3 up 8) into table 4 - x, x
+    // = the tag in bits 2s..2s+1: next state 9 x (3 - x), and x = 0 (no predecessor) gives 27
+    // (stop) -- one formula, 27 - 9x, for every x.  The three 2-bit tags spread to 9-bit
+    // spacing by one multiply (copies at bits 0, 7, 14 never overlap), then the word is
+    // C - 144 x spread (each field 27 - 9x >= 0: no borrow between fields).
+    constexpr unsigned C = 9u | (1u << 9) | (8u << 18) | (27u << 4) | (27u << 13) | (27u << 22) | (1u << 31);
+    const unsigned sp = (dv * 0x4081u) & 0xC0603u;
+    return C - 144u * sp;
+  } else if constexpr (KIND == TB_REF) {
+    // table numbers x = 1..3 (0: no predecessor): next state 9 (x - 1), or 27
+    auto fld = [](unsigned step, unsigned x) { return step | ((x ? 9u * (x - 1u) : 27u) << 4); };
+    return fld(9u, dv & 3u) | (fld(1u, (dv >> 2) & 3u) << 9) | (fld(8u, (dv >> 4) & 3u) << 18) | (1u << 31);
+  } else {
+    const unsigned fH = (unsigned)(TB_FH >> (16 * (dv & 3u))) & 0x1ffu;
+    const unsigned fE = 1u | ((dv & 4u) ? 0u : (9u << 4));
+    const unsigned fF = 8u | ((dv & 8u) ? 0u : (18u << 4));
+    return fH | (fE << 9) | (fF << 18) | (1u << 31);
+  }
+}
+
+// KIND TB_SW: Smith-Waterman affine walk; TB_REF / TB_REF_TAG: the reference's Gotoh walk
+// (end_type, h: find_alignment's end rule).
+template <int KIND>
 __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict__ dir,
                                                        const msa_pair_desc* __restrict__ pairs,
                                                        const msa_stripe_meta* __restrict__ meta,
                                                        const PairResult* __restrict__ res, int pair, int end_type,
-                                                       int hpen, int tagdir, uint8_t* __restrict__ ops, long long cap,
+                                                       int hpen, uint8_t* __restrict__ ops, long long cap,
                                                        long long* __restrict__ info) {
+  constexpr bool REF = KIND != TB_SW;
   const int lane = threadIdx.x;
   const msa_pair_desc pd = pairs[pair];
   const PairResult r0 = res[pair];
@@ -111,7 +144,12 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
   int st = 0;
   if constexpr (REF) st = ref_end_state(r0.fin, end_type, hpen);
   int status = 0;
-  __shared__ __attribute__((aligned(16))) uint8_t stage[2][4096];  // current group / the one being fetched
+  // current group / the one being fetched, behind a guard: a window lane whose cell lies
+  // outside the group reads an unused byte (down to 1,136 B before a buffer), never another
+  // variable (its word is never reached: the step budget keeps the walk inside the group)
+  constexpr int TB_GUARD = 1280;
+  __shared__ __attribute__((aligned(16))) uint8_t stage_raw[TB_GUARD + 2 * 4096];
+  uint8_t (*stage)[4096] = reinterpret_cast<uint8_t (*)[4096]>(stage_raw + TB_GUARD);
   typedef __attribute__((address_space(3))) uint8_t lds_u8;
   const unsigned stage_lds = (unsigned)(uintptr_t)(lds_u8*)&stage[0][0];
   int cb = 0;  // stage[cb] holds the current group, stage[cb ^ 1] receives the next
@@ -174,12 +212,16 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
 #ifdef MSA_TB_STATS
   long long n_outer = 0, n_win = 0, t_win = 0;  // diagnostic build: outer iterations, windows, ticks in windows
 #endif
-  long long t_wait = 0;                        // clock ticks spent waiting for group loads
+  long long t_wait = 0;  // diagnostic build: clock ticks spent waiting for group loads
   const long long t_begin = (long long)__builtin_amdgcn_s_memtime();
   auto timed_wait = [&]() {
+#ifdef MSA_TB_STATS
     const long long a = (long long)__builtin_amdgcn_s_memtime();
     vm_wait_all();
     t_wait += (long long)__builtin_amdgcn_s_memtime() - a;
+#else
+    vm_wait_all();
+#endif
   };
   if (REF || r0.score > 0) {
     bool stopped = false;
@@ -239,16 +281,18 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
         nxt_key = want;
         pend = true;
       }
-      const uint8_t* grp = &stage[cb][0];
       const int r_in = r, t_in = t;
       // The budget's steps run in windows of up to 7.  One LDS read gives lane (a, b) =
       // (lane >> 3, lane & 7) the direction byte of cell (i - a, j - b) -- (r - a, t - a - b) in
-      // the group -- and the lane turns it into a transition word: for each state s (bits 9s..)
-      // the lane step of the move (4 bits: 9 M, 1 D, 8 I, 0 none) and 9 x the next state (5
-      // bits; 27 = local start, stop), in the oracle's tie order (tb_lut).  A step is then a
-      // v_readlane of the word at the walk's lane index plus four scalar ops; seven steps stay
-      // inside the 8 x 8 window, the budget keeps them inside the group.
-      const int wa = lane >> 3, wb = lane & 7;
+      // the group -- and the lane turns it into its transition word (tb_word).  A step is then
+      // a v_readlane of the word at the walk's lane index plus a few scalar ops; seven steps
+      // stay inside the 8 x 8 window, the budget keeps them inside the group.
+      // The byte of (rr, tt) sits at ((tt >> 4) << 10) | (rr << 4) | (tt & 15) of the group.
+      // With u = t & 15 and d = u - (a + b) in [-14, 15]: tt >> 4 = (t >> 4) + (d >> 4) and
+      // tt & 15 = d & 15, so the address is a uniform part plus d + 1008 (d >> 4) - 16a (lanes
+      // outside the group land in the guard or an unused byte, never reached).
+      const unsigned grp_lds = stage_lds + 4096u * (unsigned)cb;
+      const int wc = (lane >> 3) + (lane & 7), wa16 = 16 * (lane >> 3);
       bool stop = false;
 #ifdef MSA_TB_STATS
       ++n_outer;
@@ -257,56 +301,37 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
       int sh = 9 * st;
       while (budget > 0 && !stop) {
         const int kmax = budget < 7 ? budget : 7;
-        const int rr = r - wa, tt = t - wa - wb;
-        const bool in_grp = rr >= 0 && (tt >> 6) == (t >> 6);
-        // every lane reads (a clamped address when its cell is outside the group): no
-        // exec-mask branch around the LDS read
-        const int ga = in_grp ? ((((tt >> 4) & 3) << 10) | (rr << 4) | (tt & 15)) : 0;
-        unsigned raw = grp[ga];
-        asm("" : "+v"(raw));  // keep the read unconditional
-        const unsigned dv = in_grp ? raw : 0u;
-        int wt;
-        if constexpr (REF) {
-          // table s (T1, T2, T3) leaves by its fixed move (diagonal 9, left 1, up 8) into the
-          // table bits 2s..2s+1 name; 0 there (no predecessor) stops the walk with an error
-          // (tagdir: the tagged-max fill stores tag 4 - table; 0 stays "no predecessor")
-          auto fld = [&](unsigned step, unsigned x) {
-            const unsigned nt = (tagdir && x) ? 4u - x : x;
-            return step | ((nt ? 9u * (nt - 1u) : 27u) << 4);
-          };
-          wt = (int)(fld(9u, dv & 3u) | (fld(1u, (dv >> 2) & 3u) << 9) | (fld(8u, (dv >> 4) & 3u) << 18));
-        } else {
-          const unsigned fH = (unsigned)(TB_FH >> (16 * (dv & 3u))) & 0x1ffu;
-          const unsigned fE = 1u | ((dv & 4u) ? 0u : (9u << 4));
-          const unsigned fF = 8u | ((dv & 8u) ? 0u : (18u << 4));
-          wt = (int)(fH | (fE << 9) | (fF << 18));
-        }
+        const int tg = t & 63;
+        const int d = (tg & 15) - wc;
+        const unsigned ga = grp_lds + (unsigned)(((tg >> 4) << 10) + (r << 4)) + (unsigned)(d + 1008 * (d >> 4) - wa16);
+        const unsigned dv = *(const lds_u8*)(uintptr_t)ga;
+        const int wt = (int)tb_word<KIND>(dv);
         int idx = 0, k = 0;
         unsigned wcode = 0;
         if (kmax == 7) {
-          // a full window (the common case), unrolled: per step a v_readlane and five scalar
-          // ops, and a stop test that is taken once per traceback (the runtime-bounded loop
-          // below compiles to ~25 scalar instructions and two branches per step)
+          // a full window (the common case), unrolled and branch-free: per step a v_readlane,
+          // a 64-bit shift (the absorbing stop, tb_word) and five scalar ops
 #pragma unroll
           for (int kk = 0; kk < 7; ++kk) {
-            const unsigned f = (unsigned)__builtin_amdgcn_readlane(wt, idx) >> sh;
+            const unsigned long long w64 = (13ull << 32) | (unsigned)__builtin_amdgcn_readlane(wt, idx);
+            const unsigned f = (unsigned)(w64 >> sh);
             const unsigned dl = f & 15u;
             sh = (int)((f >> 4) & 31u);
             idx += (int)dl;
             wcode |= dl << (4 * kk);
-            k = kk + 1;
-            if (sh == 27) { stop = true; break; }
           }
+          k = 7;
         } else {
           for (; k < kmax; ++k) {
-            const unsigned f = (unsigned)__builtin_amdgcn_readlane(wt, idx) >> sh;
+            const unsigned long long w64 = (13ull << 32) | (unsigned)__builtin_amdgcn_readlane(wt, idx);
+            const unsigned f = (unsigned)(w64 >> sh);
             const unsigned dl = f & 15u;
             sh = (int)((f >> 4) & 31u);
             idx += (int)dl;
             wcode |= dl << (4 * k);
-            if (sh == 27) { ++k; stop = true; break; }
           }
         }
+        stop = sh == 27;  // the steps after a stop recorded no-op nibbles
         rawl[nw] = wcode | ((unsigned)k << 28);  // every lane stores the same word
         if (++nw == TB_RAW) decode();
         const int da = idx >> 3, db = idx & 7;
