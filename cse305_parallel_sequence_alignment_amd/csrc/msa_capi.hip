@@ -305,6 +305,8 @@ kfn_t pick_kernel(int alg, int out, int tp, bool sgl) {
 
 // single-pair SW linear (msa_flow.hip): pass 1 (chain), pass 2 (fill + H)
 kfn_t pick_flow(int alg, bool best, bool save, int tp, int R) {
+  // SW affine (direction bytes): pass 1 + in-launch pass 2, one row per lane
+  if (alg == MSA_ALG_SWA) return (save && R == 1) ? flow_kernel<true, false, true, true, 1, true> : nullptr;
   // score-only plans: pass 1 alone, one row per lane, best cell tracked in the chain;
   // H plans: pass 1 + in-launch pass 2, two rows per lane
   const bool fl = (alg == MSA_ALG_SWL);
@@ -507,13 +509,22 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   const bool single = desc->single != 0;
   P->d.single = single ? 1 : 0;
   // flow kernels: one SW-linear pair whose 8 LDS code copies fit next to the rings
-  // (n <= ~19.5k columns); wider pairs run the one-pass stripe kernel
-  const size_t flow_lds = (size_t)(FL_FLAGS + (FL_W + 1) * 256) * 4 + (size_t)FL_NCOPY * fl_code_bytes((int)desc->n[0]);
-  const bool flow = single && (kalg == MSA_ALG_SWL || kalg == MSA_ALG_SWL0) &&
-                    (out_mode == MSA_OUT_H || (out_mode == MSA_OUT_NONE && !tp)) && desc->m[0] > 0 &&
-                    flow_lds <= 160 * 1024;
+  // (n <= ~19.5k columns), or one SW-affine pair with direction bytes (two values per link
+  // column, 4 code copies: n <= ~37k); wider pairs run the one-pass stripe kernel
+  const bool aff = kalg == MSA_ALG_SWA;
+  const size_t flow_lds = (size_t)(FL_FLAGS + (FL_W + 1) * 256 * (aff ? 2 : 1)) * 4 +
+                          (size_t)(aff ? 4 : FL_NCOPY) * fl_code_bytes((int)desc->n[0]);
+  // affine: profile bytes score + 2e + (o - e) must be int8
+  const bool aff_ok = aff && out_mode == MSA_OUT_DIR && desc->gap_extend >= 0 &&
+                      desc->gap_open >= desc->gap_extend &&
+                      std::max(desc->match, desc->mismatch) + desc->gap_open + desc->gap_extend <= 127 &&
+                      std::min(desc->match, desc->mismatch) + desc->gap_open + desc->gap_extend >= -128 &&
+                      (int64_t)desc->gap_extend * (desc->m[0] + desc->n[0] + 2) < (int64_t(1) << 28);
+  const bool flow = single && ((kalg == MSA_ALG_SWL || kalg == MSA_ALG_SWL0) ?
+                               (out_mode == MSA_OUT_H || (out_mode == MSA_OUT_NONE && !tp)) : aff_ok) &&
+                    desc->m[0] > 0 && flow_lds <= 160 * 1024;
   P->flow = flow;
-  P->flow2 = flow && out_mode == MSA_OUT_H;
+  P->flow2 = flow && (out_mode == MSA_OUT_H || aff);
   const int W = flow ? FL_W : (single ? MSA_WAVES_SINGLE : MSA_WAVES_BATCH);
   P->W = W;
   const int KS = flow ? 16 : (single ? ks_single(kalg) : MSA_KS_BATCH);
@@ -521,7 +532,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   P->threads = (flow ? W + 2 : W + 1 + (single ? 1 : 0)) * 64;
   // rows per lane of the flow kernel (two-pass plans): 2 halves the inter-wave hand-offs per row
   P->R = (flow && out_mode == MSA_OUT_H) ? 2 : 1;
-  P->fn = flow ? pick_flow(kalg, out_mode == MSA_OUT_NONE, out_mode == MSA_OUT_H, tp, P->R)
+  P->fn = flow ? pick_flow(kalg, out_mode == MSA_OUT_NONE, P->flow2, tp, P->R)
                : pick_kernel(kalg, out_mode, tp, single);
   if (!P->fn) { delete P; return MSA_ERR_UNSUPPORTED; }
   P->nc = nc_of(kalg);
@@ -657,7 +668,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     kp.lds_code_bytes = fl_code_bytes((int)desc->n[0]);
     P->lds_bytes = flow_lds;
     // pass-2 blocks: 544 ints per wave past the flags
-    if (out_mode == MSA_OUT_H) P->lds_bytes = std::max(flow_lds, (size_t)(FL_FLAGS + (FL_W + 2) * 544) * 4);
+    if (P->flow2) P->lds_bytes = std::max(flow_lds, (size_t)(FL_FLAGS + (FL_W + 2) * 544) * 4);
   }
   if (P->lds_bytes > 160 * 1024) {
     std::fprintf(stderr, "msa: problem needs %zu B of LDS per workgroup (> 160 KiB)\n", P->lds_bytes);
@@ -778,8 +789,9 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
       key[b] = (P->R == 2 ? 7.5 : 6.5) * (b / P->nseg) + (double)FL_PS * (b % P->nseg + 1);
     }
     std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return key[x] < key[y]; });
-    const size_t brb = sizeof(unsigned long long) * (size_t)S * P->brw;
-    const size_t snb = sizeof(unsigned long long) * (size_t)P->nblk * 128 * P->R;
+    // (affine: the F~ bottom rows follow the Z rows; a snapshot is 4 values per lane)
+    const size_t brb = sizeof(unsigned long long) * (size_t)S * P->brw * (P->kp.alg == MSA_ALG_SWA ? 2 : 1);
+    const size_t snb = sizeof(unsigned long long) * (size_t)P->nblk * (P->kp.alg == MSA_ALG_SWA ? 256 : 128 * P->R);
     if (!P->alloc(&P->d_br, brb) || hipMemset(P->d_br, 0, brb) != hipSuccess) return fail();
     if (!P->alloc(&P->d_snap, snb) || hipMemset(P->d_snap, 0, snb) != hipSuccess) return fail();
     if (!P->alloc(&P->d_blk, sizeof(int4) * (size_t)P->nblk)) return fail();

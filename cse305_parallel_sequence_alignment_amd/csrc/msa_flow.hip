@@ -162,6 +162,55 @@ __device__ __forceinline__ void ds_handoff_tid(unsigned long long m63, unsigned 
       : "memory");
 }
 
+// Affine hand-off: lane 63 alone writes its 16 Z and 16 F~ of the phase as 8 b128 writes
+// (the F~ half of a link's ring sits 1 KiB after the Z half), then the phase counter.
+__device__ __forceinline__ void ds_handoff_aff(unsigned long long m63, unsigned addr, const fl_v4i (&z)[4],
+                                               const fl_v4i (&f)[4], unsigned pa, int pv) {
+  unsigned long long sv;
+  asm volatile(
+      "s_mov_b64 %[sv], exec\n\ts_mov_b64 exec, %[m]\n\ts_nop 0\n\t"
+      "ds_write_b128 %[a], %[z0]\n\tds_write_b128 %[a], %[z1] offset:16\n\t"
+      "ds_write_b128 %[a], %[z2] offset:32\n\tds_write_b128 %[a], %[z3] offset:48\n\t"
+      "ds_write_b128 %[a], %[f0] offset:1024\n\tds_write_b128 %[a], %[f1] offset:1040\n\t"
+      "ds_write_b128 %[a], %[f2] offset:1056\n\tds_write_b128 %[a], %[f3] offset:1072\n\t"
+      "ds_write_b32 %[pa], %[pv]\n\t"
+      "s_mov_b64 exec, %[sv]\n\ts_nop 4"
+      : [sv] "=&s"(sv)
+      : [m] "s"(m63), [a] "v"(addr), [z0] "v"(z[0]), [z1] "v"(z[1]), [z2] "v"(z[2]), [z3] "v"(z[3]), [f0] "v"(f[0]),
+        [f1] "v"(f[1]), [f2] "v"(f[2]), [f3] "v"(f[3]), [pa] "v"(pa), [pv] "v"(pv)
+      : "memory");
+}
+typedef unsigned fl_v2u __attribute__((ext_vector_type(2)));
+// 16 code bytes from a 4-byte aligned LDS address: two ds_read2_b32
+__device__ __forceinline__ void ds_read_codes16(unsigned a, fl_v2u& lo, fl_v2u& hi) {
+  asm volatile("ds_read2_b32 %0, %2 offset1:1\n\tds_read2_b32 %1, %2 offset0:2 offset1:3"
+               : "=&v"(lo), "=&v"(hi)
+               : "v"(a)
+               : "memory");
+}
+template <int N = 0>
+__device__ __forceinline__ void lgkm_wait_aff(fl_v4i (&z)[4], fl_v4i (&f)[4], fl_v2u& lo, fl_v2u& hi) {
+  asm volatile("s_waitcnt lgkmcnt(%10)"
+               : "+v"(z[0]), "+v"(z[1]), "+v"(z[2]), "+v"(z[3]), "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]),
+                 "+v"(lo), "+v"(hi)
+               : "i"(N)
+               : "memory");
+}
+// Affine profile: score + 2e + oe for codes 0..6 (int8); the virtual code 7 gets 0, i.e. s =
+// -(2e + oe) <= 0, which keeps H = 0 left of column 1 and never lifts a cell right of n
+// above the real cell it came from.
+__device__ __forceinline__ void fl_profile_aff(int match, int mismatch, int e, int oe, unsigned ac, unsigned& plo,
+                                               unsigned& phi) {
+  const int sm = match + 2 * e + oe, sx = mismatch + 2 * e + oe;
+  const unsigned bx = (unsigned)(sx & 0xff) * 0x01010101u;
+  unsigned lo = bx, hi = bx;
+  const unsigned bm = (unsigned)(sm & 0xff);
+  if (ac < 4) lo = (lo & ~(0xffu << (8 * ac))) | (bm << (8 * ac));
+  else hi = (hi & ~(0xffu << (8 * (ac - 4)))) | (bm << (8 * (ac - 4)));
+  plo = lo;
+  phi = hi & 0x00ffffffu;
+}
+
 // Substitution profile of a row: score + g (X-space) or + 2g (G-space) for
 // codes 0..7; code 7 = virtual column (outside [1, n]): score 0 without the
 // floor (keeps H = 0 left of column 1, never above a real cell right of n),
@@ -196,6 +245,16 @@ __device__ __forceinline__ int fl_step(int in, int s, int& X, int& U, int g) {
 // FLOOR: scores may be negative (zero floor, X-space); otherwise G-space.
 // BEST: track the best cell in pass 1 (score-only plans: no pass 2).
 // SAVE: write BR and SNAP for pass 2.
+// AFF: Smith-Waterman with affine gaps (config C5), pass 2 writing direction bytes.  Values
+// run shifted by e(i+j) (e = gap_extend, o = gap_open, oe = o - e):
+//   H~ = H + e(i+j),  E~ = E + e(i+j),  F~ = F + e(i+j),  Z = H~ - oe
+//   E~(i,j) = max(E~(i,j-1), Z(i,j-1))      F~(i,j) = max(F~(i-1,j), Z(i-1,j))
+//   H~(i,j) = max(Z(i-1,j-1) + s + 2e + oe,  E~,  F~,  e(i+j))
+// so no gap constant sits between a DPP and its max; the floor e(i+j) is wave-uniform per
+// step (i+j is constant along a step).  Lanes hand Z and F~ down (2 DPPs per step), links
+// carry both (two values per column in the rings, granules and bottom rows), a lane's state
+// is (Z left, E~, F~, diagonal Z).  The direction byte is stripe_kernel's MSA_ALG_SWA byte:
+// every tie test compares values at one cell, which the shift leaves exact.
 // What a pass-2 block needs, by value (a reference to the kernel's KArgs would
 // put them on the stack of the pass-1 path too).
 struct FillArgs {
@@ -209,14 +268,20 @@ struct FillArgs {
   long long cod_copy, a_off, cod_off, out_off;
   int m, n, pmax, nseg, brw, match, mismatch, g;
   unsigned ep;
+  uint8_t* outDir;  // affine: direction bytes
+  int oe;           // affine: gap_open - gap_extend (g = gap_extend)
 };
 template <bool FLOOR, bool TRACKPOS, int R>
 __device__ __attribute__((noinline)) void fill_block(const FillArgs f, int blk, int lane, int* lds);
+__device__ __attribute__((noinline)) void fill_block_aff(const FillArgs f, int blk, int lane, int* lds);
 
-template <bool FLOOR, bool BEST, bool SAVE, bool TRACKPOS, int R = 1>
+template <bool FLOOR, bool BEST, bool SAVE, bool TRACKPOS, int R = 1, bool AFF = false>
 __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
   constexpr bool GS = !FLOOR;
   static_assert(R == 1 || (R == 2 && !BEST), "two rows per lane: pass-2 plans only");
+  static_assert(!AFF || (R == 1 && SAVE && !BEST), "affine: two-pass, one row per lane");
+  constexpr int NV = AFF ? 2 : 1;                  // values per column on a link (Z, F~)
+  constexpr int NCP = AFF ? 4 : FL_NCOPY;          // LDS code copies (affine: 4-byte aligned reads)
   extern __shared__ __attribute__((aligned(16))) int smem[];
   const msa_kparams& kp = a.kp;
   const int lane = threadIdx.x & 63;
@@ -226,13 +291,14 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
   // compute wave c's finished phases); rcons[l] 64+l (io-out: blocks of link l
   // taken); dummy sink 96..127
   int* flags = smem;
-  int* rings = smem + FL_FLAGS;                                          // [W+1 links][256]
-  uint8_t* codes = reinterpret_cast<uint8_t*>(rings + (W + 1) * 256);  // [8][L8]
+  int* rings = smem + FL_FLAGS;                                               // [W+1 links][NV][256]
+  uint8_t* codes = reinterpret_cast<uint8_t*>(rings + (W + 1) * 256 * NV);  // [NCP][L8]
   const int L8 = kp.lds_code_bytes;
   const msa_pair_desc pd = a.pairs[0];
   const int m = pd.m, n = pd.n;
   const int S = (m + 64 * R - 1) / (64 * R);
   const int g = kp.gap_ext;
+  const int oe = kp.gap_open - kp.gap_ext;  // affine
   const unsigned ep = kp.epoch;
   const int grp = (int)(blockIdx.x & 7), chunk = kp.sched_cap;
 
@@ -255,8 +321,10 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         if (t >= a.nblk) break;
         const FillArgs f{a.A, a.cod, a.br, a.snap, a.outH, a.blk, a.err, a.cod_copy, a.pairs[0].a_off,
                          a.pairs[0].cod_off, a.pairs[0].out_off, a.pairs[0].m, a.pairs[0].n, a.pairs[0].pmax,
-                         a.nseg, a.brw, kp.match, kp.mismatch, kp.gap_ext, kp.epoch};
-        fill_block<FLOOR, TRACKPOS, R>(f, a.border[t], lane, smem + w * 544);
+                         a.nseg, a.brw, kp.match, kp.mismatch, kp.gap_ext, kp.epoch, a.outDir,
+                         kp.gap_open - kp.gap_ext};
+        if constexpr (AFF) fill_block_aff(f, a.border[t], lane, smem + w * 544);
+        else fill_block<FLOOR, TRACKPOS, R>(f, a.border[t], lane, smem + w * 544);
       }
       return;
     }
@@ -296,55 +364,61 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
       int Yr = 0;  // bytes [0, Yr) of every LDS code copy are loaded
       auto load_codes = [&](int Y1) __attribute__((always_inline)) {
         Y1 = min(Y1, L8);
-        const int tot = FL_NCOPY * ((Y1 - Yr) / 16);  // 16-byte chunks over all copies
+        const int tot = NCP * ((Y1 - Yr) / 16);  // 16-byte chunks over all copies
         for (int c0 = 0; c0 < tot; c0 += 4 * 64) {     // 4 loads in flight per lane
           int4 v[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int c = min(c0 + r * 64 + lane, tot - 1);
-            const int x = c & (FL_NCOPY - 1), y = Yr + 16 * (c >> 3);
+            const int x = c & (NCP - 1), y = Yr + 16 * (c / NCP);
             v[r] = *reinterpret_cast<const int4*>(gcod + (size_t)x * a.cod_copy + (y + MSA_CPAD - 1 - FL_OFF));
           }
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int c = c0 + r * 64 + lane;
-            const int x = c & (FL_NCOPY - 1), y = Yr + 16 * (c >> 3);
+            const int x = c & (NCP - 1), y = Yr + 16 * (c / NCP);
             if (c < tot) *(lds_int4*)(codes + x * L8 + y) = fl_v4i{v[r].x, v[r].y, v[r].z, v[r].w};
           }
         }
         Yr = max(Yr, Y1);
       };
       load_codes(1024);
-      const unsigned long long* g_in = a.gbuf + (size_t)(item > 0 ? item - 1 : 0) * a.gbuf_stride;
+      const unsigned long long* g_in = a.gbuf + (size_t)(item > 0 ? item - 1 : 0) * NV * a.gbuf_stride;
       int b = 0;
       int consv = 0;
       unsigned spins = 0;
       while (b <= Bmax) {
         if (Yr < L8 && Yr < 16 * b + 768) load_codes(Yr + 1024);
         // up to 16 blocks (256 columns) per round trip: lane l, load r -> block b + 4r + l/16
-        int val[4];
+        int val[4], valf[4];
         int nb = 0;
         if (k0 == 0) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int col = cs_c + 16 * b + 64 * r + lane;
-            val[r] = GS ? g * col : -g;  // row 0: H = 0
+            val[r] = AFF ? g * col - oe : (GS ? g * col : -g);  // row 0: H = 0 (affine: Z; F~ = -inf)
+            valf[r] = MSA_NEG;
           }
           nb = min(16, Bmax - b + 1);
         } else {
-          unsigned long long gv[4];
+          unsigned long long gv[4], gf[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int col = cs_c + 16 * b + 64 * r + lane;
             const int ci = min(max(col + MSA_GOFF, 0), a.gbuf_stride - 1);
             gv[r] = gload(g_in + ci);
+            if constexpr (AFF) gf[r] = gload(g_in + a.gbuf_stride + ci);
           }
           bool run = true;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             val[r] = (int)(unsigned)gv[r];
             const int blk = b + 4 * r + (lane >> 4);
-            const bool ok = (blk > Bmax) || ((unsigned)(gv[r] >> 32) == ep);
+            bool ok = (blk > Bmax) || ((unsigned)(gv[r] >> 32) == ep);
+            if constexpr (AFF) {
+              valf[r] = (int)(unsigned)gf[r];
+              ok = ok && ((blk > Bmax) || ((unsigned)(gf[r] >> 32) == ep));
+            }
             const unsigned long long bal = __ballot(ok);
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj) {
@@ -367,7 +441,10 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int blk = b + 4 * r + (lane >> 4);
-          if (blk < b + nb) *L(ring + (blk & (FL_RINGB - 1)) * 16 + (lane & 15)) = val[r];
+          if (blk < b + nb) {
+            *L(ring + (blk & (FL_RINGB - 1)) * 16 + (lane & 15)) = val[r];
+            if constexpr (AFF) *L(ring + 256 + (blk & (FL_RINGB - 1)) * 16 + (lane & 15)) = valf[r];
+          }
         }
         FL_CBAR();
         if (lane == 0) lds_vstore(pub, b + nb);
@@ -381,7 +458,8 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         bl[l] = 0;
         bmx[l] = (l >= 1 && k0 + l < S && (SAVE || l == W)) ? fl_bmax(k0 + l, m, n, R) : -1;
       }
-      unsigned long long* g_out = a.gbuf + (size_t)item * a.gbuf_stride;
+      unsigned long long* g_out = a.gbuf + (size_t)item * NV * a.gbuf_stride;
+      const int S_br = (m + 64 * R - 1) / (64 * R);  // affine: F~ bottom rows follow the Z rows
       unsigned spins = 0;
       for (;;) {
         bool left = false, any = false;
@@ -398,12 +476,21 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
           const int j = lane >> 4, c = lane & 15;
           if (j < nb) {
             const int blk = bl[l] + j;
-            const int v = *(const lds_int*)(rings + l * 256 + (blk & (FL_RINGB - 1)) * 16 + c);
-            if (SAVE) gstore(a.br + (size_t)(kc - 1) * a.brw + 16 * blk + c, ((unsigned long long)ep << 32) | (unsigned)v);
+            const int v = *(const lds_int*)(rings + l * 256 * NV + (blk & (FL_RINGB - 1)) * 16 + c);
+            const int vf = AFF ? *(const lds_int*)(rings + l * 256 * NV + 256 + (blk & (FL_RINGB - 1)) * 16 + c) : 0;
+            if (SAVE) {
+              gstore(a.br + (size_t)(kc - 1) * a.brw + 16 * blk + c, ((unsigned long long)ep << 32) | (unsigned)v);
+              if constexpr (AFF)
+                gstore(a.br + (size_t)(S_br + kc - 1) * a.brw + 16 * blk + c,
+                       ((unsigned long long)ep << 32) | (unsigned)vf);
+            }
             if (l == W) {
               const int col = fl_cs(kc) + 16 * blk + c;
-              if (col + MSA_GOFF >= 0 && col + MSA_GOFF < a.gbuf_stride)
+              if (col + MSA_GOFF >= 0 && col + MSA_GOFF < a.gbuf_stride) {
                 gstore(g_out + col + MSA_GOFF, ((unsigned long long)ep << 32) | (unsigned)v);
+                if constexpr (AFF)
+                  gstore(g_out + a.gbuf_stride + col + MSA_GOFF, ((unsigned long long)ep << 32) | (unsigned)vf);
+              }
             }
           }
           bl[l] += nb;
@@ -417,6 +504,190 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         }
       }
     } else if (k0 + w < S) {
+     if constexpr (AFF) {
+      // =================== compute wave (affine): stripe k ===================
+      const int k = k0 + w;
+      const int cs = fl_cs(k);
+      const int P = fl_P(k, m, n, 1);
+      const int row_i = 64 * k + lane + 1;
+      const unsigned ac = (row_i <= m) ? (a.A[pd.a_off + row_i - 1] & 7u) : 0u;
+      const bool has_out = (k < S - 1);
+      const int Bin = (k == 0) ? P - 1 : min(P - 1, fl_bmax(k, m, n, 1));
+      const int dq_in = (w == 0) ? 0 : fl_dq(k);
+      const int dq = has_out ? fl_dq(k + 1) : 0;
+      const unsigned a_ring_in = lds_addr(rings + w * 512);
+      const unsigned a_prog_in = lds_addr(flags + 32 + w);
+      const unsigned a_ring_out = lds_addr(rings + (w + 1) * 512);
+      int* const prog_me = flags + 32 + w + 1;
+      const unsigned a_prog_me = lds_addr(prog_me);
+      const unsigned a_cons1 = lds_addr(w + 1 < W ? flags + 32 + w + 2 : flags + 64 + W);
+      const unsigned a_cons2 = lds_addr(flags + 64 + w + 1);
+      unsigned plo, phi;
+      fl_profile_aff(kp.match, kp.mismatch, g, oe, ac, plo, phi);
+      unsigned a_code;
+      {
+        const int c0 = cs - lane + FL_OFF;
+        const int x = c0 & (NCP - 1);
+        a_code = lds_addr(reinterpret_cast<int*>(codes + x * L8 + (c0 - x)));
+      }
+      // step 0: lane r at column cs - r (virtual, H = 0): its left cell's Z, the diagonal Z
+      const int flr0 = g * (64 * k + 1 + cs);  // e(i+j) at step 0, every lane
+      int Zl = g * (row_i + cs - lane - 1) - oe;
+      int U = Zl - g;
+      int E = MSA_NEG, Fo = MSA_NEG;
+      int pubv = 0, consv = 0;
+      unsigned spins = 0;
+      fl_v4i ZA[4], FA[4], ZB[4], FB[4];
+      fl_v2u CAl, CAh, CBl, CBh;
+      const unsigned long long m63 = 1ull << 63;
+      auto issue_reads = [&](int q, fl_v4i (&Z)[4], fl_v4i (&F)[4], fl_v2u& Cl, fl_v2u& Ch, int& pubn)
+          __attribute__((always_inline)) {
+        const unsigned ra = a_ring_in + (unsigned)((q & (FL_RINGB - 1)) * 64);
+        pubn = ds_read_b32(a_prog_in);
+        Z[0] = ds_read_b128<0>(ra);
+        Z[1] = ds_read_b128<16>(ra);
+        Z[2] = ds_read_b128<32>(ra);
+        Z[3] = ds_read_b128<48>(ra);
+        F[0] = ds_read_b128<1024>(ra);
+        F[1] = ds_read_b128<1040>(ra);
+        F[2] = ds_read_b128<1056>(ra);
+        F[3] = ds_read_b128<1072>(ra);
+        ds_read_codes16(a_code + 16 * q, Cl, Ch);
+      };
+      auto wait_flag = [&](unsigned addr, int& val, int need) __attribute__((always_inline)) {
+        while (val < need) {
+          int v = ds_read_b32(addr);
+          lgkm_wait<0>(v);
+          val = uni(v);
+          if (val < need) {
+            __builtin_amdgcn_s_sleep(0);
+            if (++spins > FL_SPIN_MAX) { if (lane == 0) atomicExch(a.err, 12); break; }
+          }
+        }
+      };
+      auto refresh_cons = [&](int need) __attribute__((always_inline)) {
+        while (consv < need) {
+          int c1 = ds_read_b32(a_cons1);
+          int c2 = ds_read_b32(a_cons2);
+          lgkm_wait<0>(c1);
+          lgkm_wait<0>(c2);
+          consv = uni(min(c1, c2));
+          if (consv < need) {
+            __builtin_amdgcn_s_sleep(0);
+            if (++spins > FL_SPIN_MAX) { if (lane == 0) atomicExch(a.err, 13); break; }
+          }
+        }
+      };
+      auto mask_in = [&](int q, fl_v4i (&Z)[4], fl_v4i (&F)[4]) __attribute__((always_inline)) {
+        if (q > Bin) {  // past the producer's last column (all > n)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            Z[u] = fl_v4i{MSA_NEG, MSA_NEG, MSA_NEG, MSA_NEG};
+            F[u] = fl_v4i{MSA_NEG, MSA_NEG, MSA_NEG, MSA_NEG};
+          }
+        }
+      };
+      wait_flag(a_prog_in, pubv, min(1, Bin + 1) + dq_in);
+      {
+        int pub0;
+        issue_reads(0, ZA, FA, CAl, CAh, pub0);
+        lgkm_wait_aff<0>(ZA, FA, CAl, CAh);
+        lgkm_wait<0>(pub0);
+        mask_in(0, ZA, FA);
+      }
+      auto run_phase = [&](const int q, fl_v4i (&Z)[4], fl_v4i (&F)[4], fl_v2u& Cl, fl_v2u& Ch, fl_v4i (&Zn)[4],
+                           fl_v4i (&Fn)[4], fl_v2u& Cln, fl_v2u& Chn, auto MASK_) __attribute__((always_inline)) {
+        constexpr bool MASK = decltype(MASK_)::value;
+        const int need = MASK ? min(q + 1, Bin + 1) : q + 1;
+        if (pubv - dq_in < need) {
+          wait_flag(a_prog_in, pubv, need + dq_in);
+          const unsigned ra = a_ring_in + (unsigned)((q & (FL_RINGB - 1)) * 64);
+          ds_reread_b128x4(ra, Z);
+          ds_reread_b128x4(ra + 1024u, F);
+          if constexpr (MASK) mask_in(q, Z, F);
+        }
+        if (q % FL_PS == 0) {  // pass 2 restarts here: each lane's (Z left, E~, F~, diagonal Z)
+          unsigned long long* sp = a.snap + ((size_t)k * a.nseg + q / FL_PS) * 256 + lane;
+          gstore(sp, ((unsigned long long)ep << 32) | (unsigned)Zl);
+          gstore(sp + 64, ((unsigned long long)ep << 32) | (unsigned)E);
+          gstore(sp + 128, ((unsigned long long)ep << 32) | (unsigned)Fo);
+          gstore(sp + 192, ((unsigned long long)ep << 32) | (unsigned)U);
+        }
+        int xz[16], xf[16];
+        int pubn = 0;
+        const int flq = flr0 + 16 * g * q;
+        const unsigned cw[4] = {Cl.x, Cl.y, Ch.x, Ch.y};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const unsigned s4 = __builtin_amdgcn_perm(phi, plo, cw[u]);
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) {
+            const int kx = 4 * u + kk;
+            if (kx == FL_PF) issue_reads(q + 1, Zn, Fn, Cln, Chn, pubn);
+            const int sc = ((int)(s4 << (24 - 8 * kk))) >> 24;
+            const int upZ = dpp_shr1(Z[kx >> 2][kx & 3], Zl);
+            const int upF = dpp_shr1(F[kx >> 2][kx & 3], Fo);
+            const int e = imax(E, Zl);
+            const int f = imax(upF, upZ);
+            const int d = imax(U + sc, flq + g * kx);
+            int h = imax3(d, e, f);
+            asm("" : "+v"(h));
+            U = upZ;
+            E = e;
+            Fo = f;
+            Zl = h - oe;
+            xz[kx] = Zl;
+            xf[kx] = f;
+          }
+        }
+        lgkm_wait<10>(pubn);  // the counter read (oldest of the eleven) has landed
+        pubv = uni(pubn);
+        lgkm_wait_aff<0>(Zn, Fn, Cln, Chn);  // phase q+1's inputs (before the hand-off writes)
+        const int bq = q - dq;
+        if (has_out && bq >= 0) {
+          if (consv < bq - (FL_RINGB - 1)) refresh_cons(bq - (FL_RINGB - 1));
+          const fl_v4i z4[4] = {{xz[0], xz[1], xz[2], xz[3]}, {xz[4], xz[5], xz[6], xz[7]},
+                                {xz[8], xz[9], xz[10], xz[11]}, {xz[12], xz[13], xz[14], xz[15]}};
+          const fl_v4i f4[4] = {{xf[0], xf[1], xf[2], xf[3]}, {xf[4], xf[5], xf[6], xf[7]},
+                                {xf[8], xf[9], xf[10], xf[11]}, {xf[12], xf[13], xf[14], xf[15]}};
+          ds_handoff_aff(m63, a_ring_out + (unsigned)((bq & (FL_RINGB - 1)) * 64), z4, f4, a_prog_me, q + 1);
+        } else {
+          FL_CBAR();
+          if (lane == 0) lds_vstore(prog_me, q + 1);
+        }
+        if constexpr (MASK) mask_in(q + 1, Zn, Fn);
+      };
+      using T_ = std::true_type;
+      using F_ = std::false_type;
+      const int qa = max(0, min(P, Bin));
+      int q = 0;
+      for (; q + 1 < qa; q += 2) {
+        run_phase(q, ZA, FA, CAl, CAh, ZB, FB, CBl, CBh, F_{});
+        run_phase(q + 1, ZB, FB, CBl, CBh, ZA, FA, CAl, CAh, F_{});
+      }
+      if (q < qa) {
+        run_phase(q, ZA, FA, CAl, CAh, ZB, FB, CBl, CBh, F_{});
+        ++q;
+        for (; q + 1 < P; q += 2) {
+          run_phase(q, ZB, FB, CBl, CBh, ZA, FA, CAl, CAh, T_{});
+          run_phase(q + 1, ZA, FA, CAl, CAh, ZB, FB, CBl, CBh, T_{});
+        }
+        if (q < P) run_phase(q, ZB, FB, CBl, CBh, ZA, FA, CAl, CAh, T_{});
+      } else {
+        for (; q + 1 < P; q += 2) {
+          run_phase(q, ZA, FA, CAl, CAh, ZB, FB, CBl, CBh, T_{});
+          run_phase(q + 1, ZB, FB, CBl, CBh, ZA, FA, CAl, CAh, T_{});
+        }
+        if (q < P) run_phase(q, ZA, FA, CAl, CAh, ZB, FB, CBl, CBh, T_{});
+      }
+      lgkm_wait_aff<0>(ZA, FA, CAl, CAh);
+      lgkm_wait_aff<0>(ZB, FB, CBl, CBh);
+      msa_stripe_meta* md = a.meta + pd.stripe0 + k;
+      if (lane == 0) {
+        md->cs = cs;
+        md->phases = P;
+      }
+     } else {
       // =================== compute wave: stripe k ===================
       const int k = k0 + w;
       const int cs = fl_cs(k);
@@ -649,6 +920,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         md->cs = cs;
         md->phases = P;
       }
+     }
     }
     __syncthreads();
   }
@@ -822,6 +1094,151 @@ __device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, 
     }
   }
   // first max in row-major order: max score, then min row, then min column
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const int ob = __shfl_xor(bb, off), oi = __shfl_xor(bi, off), oj = __shfl_xor(bj, off);
+    if (ob > bb || (ob == bb && (oi < bi || (oi == bi && oj < bj)))) { bb = ob; bi = oi; bj = oj; }
+  }
+  if (lane == 0) a.blk[blk] = make_int4(bb, bi, bj, 0);
+}
+
+// Pass 2, affine (config C5): block (stripe s, segment seg) recomputes its FL_PS phases from
+// SNAP (Z left, E~, F~, diagonal Z per lane) and the stripe above's bottom row (Z and F~
+// granules), writes the direction bytes in the skewed stripe layout -- lane r's 16 bytes of a
+// phase are one 16-byte store, a wave's phase one contiguous 1 KiB -- and reduces its first
+// maximum H = H~ - e(i+j).  The bytes are stripe_kernel's MSA_ALG_SWA bytes (the walk
+// traceback_kernel<TB_SW> reads them unchanged).
+__device__ __attribute__((noinline)) void fill_block_aff(const FillArgs a, int blk, int lane, int* lds) {
+  const unsigned ep = a.ep;
+  const int m = a.m, n = a.n, S = (m + 63) / 64, g = a.g, oe = a.oe;
+  const int s = blk / a.nseg, seg = blk - s * a.nseg;
+  int bb = INT32_MIN, bi = 0, bj = 0;
+  if (s < S) {
+    const int P = fl_P(s, m, n, 1);
+    const int q0 = seg * FL_PS;
+    if (q0 < P) {
+      int q1 = min(P, q0 + FL_PS);
+      const int cs = fl_cs(s);
+      const int row_i = 64 * s + lane + 1;
+      const unsigned ac = (row_i <= m) ? (a.A[a.a_off + row_i - 1] & 7u) : 0u;
+      unsigned plo, phi;
+      fl_profile_aff(a.match, a.mismatch, g, oe, ac, plo, phi);
+      const int Bin = (s == 0) ? P - 1 : min(P - 1, fl_bmax(s, m, n, 1));
+      const unsigned long long* sp = a.snap + ((size_t)s * a.nseg + seg) * 256 + lane;
+      const unsigned long long* brz = a.br + (size_t)(s > 0 ? s - 1 : 0) * a.brw;
+      const unsigned long long* brf = a.br + (size_t)(S + (s > 0 ? s - 1 : 0)) * a.brw;
+      const int qb = (s > 0) ? min(q1, Bin + 1) : q0;
+      const int nv = 16 * max(0, qb - q0);  // granules per value, lane l holds l, l+64, ...
+      int Zl = 0, E = 0, Fo = 0, U = 0;
+      bool ready = (nv == 0);
+      for (int t2 = 0; !ready && t2 < (int)(FL_SPIN_MAX >> 2); ++t2) {  // the block's last granules first
+        const unsigned long long gz = gload(brz + 16 * q0 + nv - 1), gf = gload(brf + 16 * q0 + nv - 1);
+        ready = __ballot((unsigned)(gz >> 32) != ep || (unsigned)(gf >> 32) != ep) == 0;
+        if (!ready) __builtin_amdgcn_s_sleep(FL_FSLEEP);
+      }
+      if (ready) {
+        ready = false;
+        for (int tries = 0; !ready && tries < (int)FL_SPIN_MAX; ++tries) {
+          const unsigned long long x0 = gload(sp), x1 = gload(sp + 64), x2 = gload(sp + 128), x3 = gload(sp + 192);
+          bool ok = ((unsigned)(x0 >> 32) == ep) && ((unsigned)(x1 >> 32) == ep) && ((unsigned)(x2 >> 32) == ep) &&
+                    ((unsigned)(x3 >> 32) == ep);
+          Zl = (int)(unsigned)x0;
+          E = (int)(unsigned)x1;
+          Fo = (int)(unsigned)x2;
+          U = (int)(unsigned)x3;
+          for (int v = lane; v < nv; v += 64) {
+            const unsigned long long gz = gload(brz + 16 * q0 + v), gf = gload(brf + 16 * q0 + v);
+            ok = ok && ((unsigned)(gz >> 32) == ep) && ((unsigned)(gf >> 32) == ep);
+            *L(lds + v) = (int)(unsigned)gz;
+            *L(lds + 256 + v) = (int)(unsigned)gf;
+          }
+          ready = __ballot(!ok) == 0;
+          if (!ready) __builtin_amdgcn_s_sleep(8);
+        }
+      }
+      if (!ready) {
+        if (lane == 0) atomicExch(a.err, 15);
+        q1 = q0;
+      }
+      FL_CBAR();
+      const int b0 = cs - lane - 1 + MSA_CPAD;
+      const unsigned* cptr = reinterpret_cast<const unsigned*>(a.cod + (size_t)(b0 & (MSA_NCOPY - 1)) * a.cod_copy +
+                                                             a.cod_off + (b0 & ~(MSA_NCOPY - 1)));
+      const int flr0 = g * (64 * s + 1 + cs);
+      int best = INT32_MIN, bt = -1;
+      fl_v4u* dp = reinterpret_cast<fl_v4u*>(a.outDir + (size_t)a.out_off + (size_t)s * a.pmax * 1024) + lane;
+      auto ldc = [&](int q) __attribute__((always_inline)) {
+        return *reinterpret_cast<const uint4*>(cptr + 4 * min(q, P - 1));
+      };
+      uint4 cr0 = ldc(q0), cr1 = ldc(q0 + 1), cr2 = ldc(q0 + 2), cr3 = ldc(q0 + 3);
+      for (int q = q0; q < q1; ++q) {
+        const uint4 c4 = cr0;
+        cr0 = cr1;
+        cr1 = cr2;
+        cr2 = cr3;
+        cr3 = ldc(q + 4);
+        int INZ[16], INF[16];
+        if (q <= Bin) {
+          if (s == 0) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+              INZ[j] = g * (cs + 16 * q + j) - oe;
+              INF[j] = MSA_NEG;
+            }
+          } else {
+            const lds_int4* srz = reinterpret_cast<const lds_int4*>(L(lds + 16 * (q - q0)));
+            const lds_int4* srf = reinterpret_cast<const lds_int4*>(L(lds + 256 + 16 * (q - q0)));
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const fl_v4i vz = srz[u], vf = srf[u];
+              INZ[4 * u] = vz.x; INZ[4 * u + 1] = vz.y; INZ[4 * u + 2] = vz.z; INZ[4 * u + 3] = vz.w;
+              INF[4 * u] = vf.x; INF[4 * u + 1] = vf.y; INF[4 * u + 2] = vf.z; INF[4 * u + 3] = vf.w;
+            }
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 16; ++j) INZ[j] = INF[j] = MSA_NEG;
+        }
+        const unsigned cw[4] = {c4.x, c4.y, c4.z, c4.w};
+        const int flq = flr0 + 16 * g * q;
+        unsigned dw[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const unsigned s4 = __builtin_amdgcn_perm(phi, plo, cw[u]);
+          unsigned word = 0;
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) {
+            const int kx = 4 * u + kk;
+            const int sc = ((int)(s4 << (24 - 8 * kk))) >> 24;
+            const int flr = flq + g * kx;
+            const int upZ = dpp_shr1(INZ[kx], Zl);
+            const int upF = dpp_shr1(INF[kx], Fo);
+            const int e = imax(E, Zl);
+            const int f = imax(upF, upZ);
+            const int draw = U + sc;
+            int h = imax3(imax(draw, flr), e, f);
+            asm("" : "+v"(h));
+            // stripe_kernel's SWA byte: H's source (0 local start, 1 diagonal, 2 E, 3 F), bit 2
+            // E opened from H(i, j-1), bit 3 F opened from H(i-1, j)
+            const unsigned hs = (h == flr) ? 0u : (h == draw ? 1u : (h == e ? 2u : 3u));
+            const unsigned dir = hs | ((e == Zl) ? 4u : 0u) | ((f == upZ) ? 8u : 0u);
+            word |= dir << (8 * kk);
+            const int hv = h - flr;
+            if (hv > best) { best = hv; bt = 16 * q + kx; }
+            U = upZ;
+            E = e;
+            Fo = f;
+            Zl = h - oe;
+          }
+          dw[u] = word;
+        }
+        __builtin_nontemporal_store(fl_v4u{dw[0], dw[1], dw[2], dw[3]}, dp + (size_t)q * 64);
+      }
+      bb = (row_i <= m) ? best : INT32_MIN;
+      bi = row_i;
+      bj = cs + bt - lane;
+    }
+  }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
     const int ob = __shfl_xor(bb, off), oi = __shfl_xor(bi, off), oj = __shfl_xor(bj, off);

@@ -652,6 +652,38 @@ def test_c5_fill_and_device_traceback_20k(oracle, dev, LB, which):
     assert sc == r["score"] and stop == tuple(r["end"])
 
 
+@pytest.mark.parametrize("m,n", [(1, 1), (64, 1), (1, 300), (65, 70), (300, 257), (1000, 1300), (2600, 900)])
+@pytest.mark.parametrize("scoring", [(1, 0, 3, 1), (2, -3, 5, 2), (1, -1, 1, 1), (3, -2, 0, 0)])
+def test_sw_affine_flow_dir_bytes(dev, LB, m, n, scoring):
+    """The two-pass affine flow kernel (single pair, direction bytes: run_info mode 1) writes the same
+    direction byte as the one-pass stripe kernel (the same pair as a one-pair batch) at every cell of the
+    matrix, and the same score and first-maximum end cell."""
+    import torch
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+
+    rng = np.random.default_rng(m * 7 + n)
+    A = rs(rng, m)
+    B = bytes(bytearray(A[: min(m, n)]) + rs(rng, max(0, n - m)))
+    b = bytearray(B)
+    for k in rng.choice(len(b), size=max(1, len(b) // 10), replace=False):
+        b[k] = ACGT[rng.integers(4)]
+    B = bytes(b)
+    ma, mi, go, ge = scoring
+    out = []
+    for single in (True, False):
+        pl = Plan(LB.SW_AFFINE, LB.CELLS_DIR, [m], [len(B)], [0], [0], match=ma, mismatch=mi, gap_open=go,
+                  gap_extend=ge, track_end=True, single=single)
+        D = torch.empty(pl.cells_elems, dtype=torch.uint8, device=dev)
+        pl.run(_dev(A, dev), _dev(B, dev), D)
+        r = pl.results()[0]
+        info = pl.run_info()
+        out.append((pl.deskew_dir(D.cpu().numpy(), 0, pl.stripe_meta()), r["score"], tuple(r["end"]), info["mode"]))
+    (d1, s1, e1, mode1), (d0, s0, e0, _) = out
+    assert mode1 == "flow"
+    assert (s1, e1) == (s0, e0)
+    assert np.array_equal(d1[1:, 1:], d0[1:, 1:])
+
+
 @pytest.mark.parametrize("m,n", [(3000, 2900), (1500, 4100), (4097, 130)])
 @pytest.mark.parametrize("scoring", [(1, 0, 3, 1), (2, -3, 5, 2), (1, -1, 1, 1)])
 def test_device_traceback_multi_stripe(oracle, dev, LB, m, n, scoring):
