@@ -587,7 +587,11 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
           }
         }
       };
+#ifdef MSA_STAMPS
+      int nslow = 0;
+#endif
       wait_flag(a_prog_in, pubv, min(1, Bin + 1) + dq_in);
+      FL_STAMP(0, 0, __builtin_amdgcn_s_memrealtime());
       {
         int pub0;
         issue_reads(0, ZA, FA, CAl, CAh, pub0);
@@ -600,6 +604,9 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         constexpr bool MASK = decltype(MASK_)::value;
         const int need = MASK ? min(q + 1, Bin + 1) : q + 1;
         if (pubv - dq_in < need) {
+#ifdef MSA_STAMPS
+          ++nslow;
+#endif
           wait_flag(a_prog_in, pubv, need + dq_in);
           const unsigned ra = a_ring_in + (unsigned)((q & (FL_RINGB - 1)) * 64);
           ds_reread_b128x4(ra, Z);
@@ -682,6 +689,8 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
       }
       lgkm_wait_aff<0>(ZA, FA, CAl, CAh);
       lgkm_wait_aff<0>(ZB, FB, CBl, CBh);
+      FL_STAMP(0, 1, __builtin_amdgcn_s_memrealtime());
+      FL_STAMP(0, 2, (unsigned long long)nslow);
       msa_stripe_meta* md = a.meta + pd.stripe0 + k;
       if (lane == 0) {
         md->cs = cs;
@@ -1113,7 +1122,11 @@ __device__ __attribute__((noinline)) void fill_block_aff(const FillArgs a, int b
   const int m = a.m, n = a.n, S = (m + 63) / 64, g = a.g, oe = a.oe;
   const int s = blk / a.nseg, seg = blk - s * a.nseg;
   int bb = INT32_MIN, bi = 0, bj = 0;
+#ifdef MSA_AFF_NOP2
+  if (false) {  // timing variant: pass 1 alone
+#else
   if (s < S) {
+#endif
     const int P = fl_P(s, m, n, 1);
     const int q0 = seg * FL_PS;
     if (q0 < P) {

@@ -1,19 +1,21 @@
 // msa_traceback.hip -- on-device traceback walks over direction bytes.
 //
-//  * SW affine (config C5): the fill (stripe_kernel, MSA_ALG_SWA, MSA_OUT_DIR)
-//    leaves one byte per cell -- bits 0-1: where H came from (0 = local start,
-//    1 = diagonal, 2 = E / horizontal gap, 3 = F / vertical gap); bit 2: E here
-//    opened from H(i, j-1); bit 3: F here opened from H(i-1, j).  The walk is the
-//    tie order of oracle orc_sw (first maximum), from the pair's end cell.
-//  * Reference Gotoh (MSA_ALG_REF, MSA_OUT_DIR: main_alignment_function /
-//    Subproblem::find_alignment, subproblem_alignment.cpp:105-172): bits 0-1 =
-//    T1's predecessor table, 2-3 = T2's, 4-5 = T3's (1..3, the first table in
-//    the reference's order T1, T2, T3 whose value reproduces the cell by exact
-//    equality).  The walk starts at (m, n) in the end node's table (the
-//    reference's end-type rule, :112-146, from the fill's final state) and stops
-//    when i == 0 or j == 0 (:147).  One op per step = the table the step leaves
-//    from ('M' T1 / diagonal, 'D' T2 / consumes B, 'I' T3 / consumes A); the host
-//    turns them into the reference's align list (node coordinates, quirks Q1/Q2).
+//  * SW affine (config C5): the fill (stripe_kernel or the affine flow kernel,
+//    MSA_ALG_SWA, MSA_OUT_DIR) leaves one byte per cell -- bits 0-1: where H came
+//    from (0 = local start, 1 = diagonal, 2 = E / horizontal gap, 3 = F / vertical
+//    gap); bit 2: E here opened from H(i, j-1); bit 3: F here opened from H(i-1, j).
+//    The walk is the tie order of oracle orc_sw (first maximum), from the pair's end
+//    cell.
+//  * Reference Gotoh (MSA_ALG_REF / REF1, MSA_OUT_DIR: main_alignment_function /
+//    Subproblem::find_alignment, subproblem_alignment.cpp:105-172): bits 0-1 = T1's
+//    predecessor table, 2-3 = T2's, 4-5 = T3's (REF: table numbers 1..3, the first
+//    table in the reference's order T1, T2, T3 whose value reproduces the cell by
+//    exact equality; REF1: tags 4 - table).  The walk starts at (m, n) in the end
+//    node's table (the reference's end-type rule, :112-146, from the fill's final
+//    state) and stops when i == 0 or j == 0 (:147).  One op per step = the table the
+//    step leaves from ('M' T1 / diagonal, 'D' T2 / consumes B, 'I' T3 / consumes
+//    A); the host turns them into the reference's align list (node coordinates,
+//    quirks Q1/Q2).
 //
 // Both layouts are the skewed stripe layout: cell (64s + r + 1, cs_s + t - r) at
 // byte (s*pmax + t/16)*1024 + r*16 + t%16 of the pair's block -- a 16-step x
@@ -21,19 +23,29 @@
 //
 // One wave walks the path from the pair's end cell (read from the reduction's
 // PairResult on the same stream, no host round trip).  Its state is uniform
-// (SGPRs); the 4 KiB group of blocks under the walk sits in LDS and a step
-// reads its byte there at a wave-uniform address.  While walking, the wave
-// prefetches the group it will need next (the stripe above, at the column the
-// path will leave through, or the group to the left, whichever boundary comes
-// first) into a second staging buffer, so most group switches find their bytes
-// already loaded.  Inside a group, one LDS read fetches an 8x8 window of bytes
-// (one per lane) and up to 7 steps are resolved from it with v_readlane.
-// Steps are recorded as nibbles, one word per window, in an LDS ring that is
+// (SGPRs).  Inside a stripe t only decreases (every move lowers it by 1 or 2), so
+// the walk needs, per stripe, the bytes left of where it enters: a GROUP of 16
+// blocks (256 steps x 64 rows, 16 KiB) ending a little right of the entry point.
+// A diagonal path crosses a stripe in 64 steps (t drops by 128), so one group per
+// stripe usually serves.  Groups are staged in LDS by LDS-DMA, one slot per stripe
+// modulo 4: entering stripe s, the walk waits for s's group and prefetches stripe
+// s-3's group at the column a diagonal path would enter it (a misprediction --
+// after gaps -- costs an on-demand load), so the HBM latency of the next stripes
+// is covered by three stripes of walking.
+// Inside a group:
+//  * in state T1 / H, one LDS gather gives lane q the byte of cell (i - q, j - q);
+//    a ballot of "diagonal move, staying in T1 / H" and a find-first-zero give the
+//    length of the diagonal run ahead (up to 64 steps in ~10 instructions: C5's
+//    optimal path is 15 diagonal runs of ~1,300 cells between 14 gaps);
+//  * otherwise an 8 x 8 window: one LDS read gives lane (a, b) the byte of cell
+//    (i - a, j - b), turned into a transition word, and up to 7 steps are resolved
+//    from it with v_readlane.
+// Steps are recorded in an LDS ring (window words of nibbles, run words) that is
 // decoded into op bytes by the whole wave in parallel (no scalar-cache writes).
 // Output: ops from the end cell back to the start ('M' diagonal, 'D' a gap
 // consuming B, 'I' a gap consuming A), info = {n_ops, beg_i, beg_j, status,
-// group switches, of them fetched on demand (mispredicted), s_memtime ticks of
-// the walk, of them waiting for group loads}.
+// stripe groups staged, of them loaded on demand (mispredicted), s_memtime ticks of
+// the walk, of them waiting for group loads (diagnostic build)}.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -41,20 +53,12 @@
 
 namespace msa {
 
-// A "group" is 4 consecutive 16-step blocks of one stripe: steps [64g, 64g + 64)
-// of all 64 rows, 4 KiB contiguous (blocks of a stripe are consecutive in
-// memory).  Lane r holds its row's 64 bytes in 16 dwords; dword k covers steps
-// 64g + 4k .. +3.  A diagonal step lowers t by 2 and r by 1, so a group serves
-// ~32 diagonal steps and a 64-row stripe takes 1-3 groups.
-// Group loads are LDS-DMA (global_load_lds_dwordx4: each lane's 16 bytes land
-// at LDS base + 16 * lane, no VGPR destination) into the second of two 4 KiB
-// staging buffers; the walk reads its byte from the current one.  They are
-// issued as inline asm so that
-// the compiler's wait-count pass does not see them -- it would otherwise drain
-// them with vmcnt(0) in front of unrelated work.  At most one group load is in
-// flight; it is waited for explicitly (s_waitcnt vmcnt(0), memory clobber, so
-// the LDS reads that follow cannot move above it) before the staging buffer is
-// read or refilled.  M0 is written in the same statement that uses it.
+// Group loads are LDS-DMA (global_load_lds_dwordx4: each lane's 16 bytes land at
+// M0 + 16 * lane, no VGPR destination), issued as inline asm so that the
+// compiler's wait-count pass does not see them (it would drain them with vmcnt(0)
+// in front of unrelated work); they are waited for explicitly (s_waitcnt vmcnt(N),
+// memory clobber) before a slot is read.  M0 is written in the statement that uses
+// it (an SALU M0 write needs one wait state before the load).
 __device__ __forceinline__ void glds16(const uint8_t* gsrc, unsigned lds_dst) {
   unsigned keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
@@ -62,16 +66,44 @@ __device__ __forceinline__ void glds16(const uint8_t* gsrc, unsigned lds_dst) {
                : "v"(gsrc), "s"(lds_dst)
                : "memory");
 }
+// 16 consecutive 1 KiB blocks (lane base pointer g) into 16 KiB of LDS at lds_dst: 16 loads.
+// The instruction offset moves the LDS destination as well as the source (measured:
+// mbench/mb_glds.hip), so four loads share one base and one M0 (offsets 0..3 KiB) and M0
+// steps by 4 KiB per base.
+__device__ __forceinline__ void glds16x16(const uint8_t* g, unsigned lds_dst) {
+  const uint8_t* g1 = g + 4096;
+  const uint8_t* g2 = g + 8192;
+  const uint8_t* g3 = g + 12288;
+  unsigned keep;
+#define TB_L4(v)                                                                                 \
+  "global_load_lds_dwordx4 " v ", off\n\tglobal_load_lds_dwordx4 " v ", off offset:1024\n\t"     \
+  "global_load_lds_dwordx4 " v ", off offset:2048\n\tglobal_load_lds_dwordx4 " v ", off offset:3072\n\t"
+#define TB_M0 "s_add_u32 m0, m0, 0x1000\n\ts_nop 0\n\t"
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %5\n\ts_nop 0\n\t" TB_L4("%1") TB_M0 TB_L4("%2") TB_M0 TB_L4("%3")
+                   TB_M0 TB_L4("%4") "s_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(g), "v"(g1), "v"(g2), "v"(g3), "s"(lds_dst)
+               : "memory");
+#undef TB_L4
+#undef TB_M0
+}
 // Transitions of the walk (oracle orc_sw tie order), by state:
 //  H: the low two bits hs of the byte -- 0 local start (stop), 1 diagonal ('M', stay in H),
 //     2 from E (no op, go to E), 3 from F (no op, go to F);
 //  E: 'D' (a gap consuming B), back to H if bit 2 (E opened from H(i, j-1)), else stay;
 //  F: 'I' (a gap consuming A), back to H if bit 3 (F opened from H(i-1, j)), else stay.
-// A transition field is (lane step: 9 M / 1 D / 8 I / 0 none) | (9 x next state, 27 = stop)
-// << 4; TB_FH holds the four H fields at 16-bit spacing, indexed by hs.
-constexpr unsigned long long TB_FH = (27ull << 4) | (9ull << 16) | ((9ull << 4) << 32) | ((18ull << 4) << 48);
+// A transition field is (10 x next state, 30 = stop) | (lane step: 9 M / 1 D / 8 I / 0 none)
+// << 6; TB_FH holds the four H fields at 16-bit spacing, indexed by hs.
+constexpr unsigned long long TB_FH = 30ull | ((9ull << 6) << 16) | (10ull << 32) | (20ull << 48);
 
 __device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" : : : "memory"); }
+// wait until at most n VMEM ops are outstanding, n rounded down to 0, 16, 32 or 48
+__device__ __forceinline__ void vm_wait_le(int n) {
+  if (n >= 48) asm volatile("s_waitcnt vmcnt(48)" : : : "memory");
+  else if (n >= 32) asm volatile("s_waitcnt vmcnt(32)" : : : "memory");
+  else if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" : : : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
+}
 
 // find_alignment's end node table (subproblem_alignment.cpp:112-146) from the final
 // state fin = (T1, T2, T3)(m, n), MSA_NEG = -inf: end_type > 0 names it; otherwise
@@ -94,32 +126,40 @@ __device__ __forceinline__ int ref_end_state(const int32_t (&fin)[3], int end_ty
 // fill) or over tags (REF1 fill, tag = 4 - table).
 enum { TB_SW = 0, TB_REF = 1, TB_REF_TAG = 2 };
 
-// The transition word of a cell (see the window comment in traceback_kernel): three 9-bit
-// fields, field s = the lane step of leaving state s | 9 x the next state << 4 (27 = stop),
-// and bit 31 set.  With bit 31 set and 13 as the high word of the 64-bit shift in a step, the
-// stop state is absorbing: shifting by 27 yields lane step 0 and next state 27 again, so the
-// steps after a stop are no-ops and a window needs no branch per step.
+// The transition word of a cell (see the window comment in traceback_kernel): three 10-bit
+// fields, field s (bits 10s..) = 10 x the next state (30 = stop) | the lane step of leaving
+// state s << 6, and bits 30-31 = 10b.  A step shifts the 64-bit {7, word} right by the current
+// field's position and takes the low 6 bits of the result as the next position (the 64-bit
+// shift reads only those 6 bits of its shift operand: no mask op), bits 6-9 as the lane step.
+// Bits 30-35 of {7, word} read 30: the stop state is absorbing (lane step 0, stay at 30), so
+// the steps after a stop are no-ops and a window needs no branch per step.
 template <int KIND>
 __device__ __forceinline__ unsigned tb_word(unsigned dv) {
   if constexpr (KIND == TB_REF_TAG) {
     // table s leaves by its fixed move (T1 diagonal 9, T2 left 1, T3 up 8) into table 4 - x, x
-    // = the tag in bits 2s..2s+1: next state 9 x (3 - x), and x = 0 (no predecessor) gives 27
-    // (stop) -- one formula, 27 - 9x, for every x.  The three 2-bit tags spread to 9-bit
-    // spacing by one multiply (copies at bits 0, 7, 14 never overlap), then the word is
-    // C - 144 x spread (each field 27 - 9x >= 0: no borrow between fields).
-    constexpr unsigned C = 9u | (1u << 9) | (8u << 18) | (27u << 4) | (27u << 13) | (27u << 22) | (1u << 31);
-    const unsigned sp = (dv * 0x4081u) & 0xC0603u;
-    return C - 144u * sp;
+    // = the tag in bits 2s..2s+1: next state 10 (3 - x), and x = 0 (no predecessor) gives 30
+    // (stop) -- one formula, 30 - 10x, for every x.  The three 2-bit tags spread to 10-bit
+    // spacing by one multiply (copies at bits 0, 8, 16 never overlap), then the word is
+    // C - 10 x spread (each field 30 - 10x >= 0: no borrow between fields).
+    constexpr unsigned C = (30u | (9u << 6)) | ((30u | (1u << 6)) << 10) | ((30u | (8u << 6)) << 20) | (1u << 31);
+    const unsigned sp = (dv * 0x10101u) & 0x300C03u;
+    return C - 10u * sp;
   } else if constexpr (KIND == TB_REF) {
-    // table numbers x = 1..3 (0: no predecessor): next state 9 (x - 1), or 27
-    auto fld = [](unsigned step, unsigned x) { return step | ((x ? 9u * (x - 1u) : 27u) << 4); };
-    return fld(9u, dv & 3u) | (fld(1u, (dv >> 2) & 3u) << 9) | (fld(8u, (dv >> 4) & 3u) << 18) | (1u << 31);
+    // table numbers x = 1..3 (0: no predecessor): next state 10 (x - 1), or 30
+    auto fld = [](unsigned step, unsigned x) { return (x ? 10u * (x - 1u) : 30u) | (step << 6); };
+    return fld(9u, dv & 3u) | (fld(1u, (dv >> 2) & 3u) << 10) | (fld(8u, (dv >> 4) & 3u) << 20) | (1u << 31);
   } else {
-    const unsigned fH = (unsigned)(TB_FH >> (16 * (dv & 3u))) & 0x1ffu;
-    const unsigned fE = 1u | ((dv & 4u) ? 0u : (9u << 4));
-    const unsigned fF = 8u | ((dv & 8u) ? 0u : (18u << 4));
-    return fH | (fE << 9) | (fF << 18) | (1u << 31);
+    const unsigned fH = (unsigned)(TB_FH >> (16 * (dv & 3u))) & 0x3ffu;
+    const unsigned fE = (1u << 6) | ((dv & 4u) ? 0u : 10u);
+    const unsigned fF = (8u << 6) | ((dv & 8u) ? 0u : 20u);
+    return fH | (fE << 10) | (fF << 20) | (1u << 31);
   }
+}
+// State 0 (T1 / H) continues diagonally and stays in state 0 at a cell with byte dv.
+template <int KIND>
+__device__ __forceinline__ bool tb_diag_stay(unsigned dv) {
+  if constexpr (KIND == TB_REF_TAG) return (dv & 3u) == 3u;  // T1's predecessor T1 (tag 3)
+  else return (dv & 3u) == 1u;                             // T1 from T1 / H from the diagonal
 }
 
 // KIND TB_SW: Smith-Waterman affine walk; TB_REF / TB_REF_TAG: the reference's Gotoh walk
@@ -144,19 +184,13 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
   int st = 0;
   if constexpr (REF) st = ref_end_state(r0.fin, end_type, hpen);
   int status = 0;
-  // current group / the one being fetched, behind a guard: a window lane whose cell lies
-  // outside the group reads an unused byte (down to 1,136 B before a buffer), never another
-  // variable (its word is never reached: the step budget keeps the walk inside the group)
-  constexpr int TB_GUARD = 1280;
-  __shared__ __attribute__((aligned(16))) uint8_t stage_raw[TB_GUARD + 2 * 4096];
-  uint8_t (*stage)[4096] = reinterpret_cast<uint8_t (*)[4096]>(stage_raw + TB_GUARD);
+  // Group slots: 4 x 16 KiB behind a guard (window lanes whose cell lies outside the group
+  // read an unused byte there -- down to 2,270 B below a slot -- and hold frozen words).
+  constexpr int GB = 16, GT = 16 * GB, GBYTES = 1024 * GB, NSLOT = 4;
+  constexpr int TB_GUARD = 2304;
+  __shared__ __attribute__((aligned(16))) uint8_t stage_raw[TB_GUARD + NSLOT * GBYTES];
   typedef __attribute__((address_space(3))) uint8_t lds_u8;
-  const unsigned stage_lds = (unsigned)(uintptr_t)(lds_u8*)&stage[0][0];
-  int cb = 0;  // stage[cb] holds the current group, stage[cb ^ 1] receives the next
-  long long cur_key = -1, nxt_key = -1;  // s * 2^32 + g
-  bool pend = false;                     // a group load into `stage` is in flight
-  int s_cached = -1;
-  int cs = 0, cs_up = 0;
+  const unsigned stage_lds = (unsigned)(uintptr_t)(lds_u8*)&stage_raw[TB_GUARD];
   // every stripe's start column, staged in LDS once (a stripe change then costs an LDS
   // read, not a ~1 us dependent global load); pairs with more stripes read the rest from HBM
   constexpr int TB_CSL = 8192;
@@ -166,11 +200,12 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
   auto cs_of = [&](int k) {  // wave-uniform (readfirstlane: an LDS value is otherwise "divergent")
     return k < TB_CSL ? __builtin_amdgcn_readfirstlane(csl[k]) : meta[pd.stripe0 + k].cs;
   };
-  // The walk records, per window of <= 7 steps, one word: nibble k = the lane step of
-  // step k (9 'M', 1 'D', 8 'I', 0 no op), steps in bits 28-31.  The words go to an LDS
-  // ring (all lanes store the same word: no per-lane branch in the walk); when it is
-  // full, and at the end, decode() turns them into op bytes in parallel (one word per
-  // lane, a wave prefix sum of the op counts) and appends them to `ops`.
+  // The walk records one word per window -- nibble q (from the top) = the lane step of step q
+  // (9 'M', 1 'D', 8 'I', 0 no op), the step count in bits 28-31 -- or per diagonal run --
+  // 15 in bits 28-31, the run length below.  The words go to an LDS ring (all lanes store
+  // the same word: no per-lane branch in the walk); when it is full, and at the end, decode()
+  // turns them into op bytes in parallel (one word per lane, a wave prefix sum of the op
+  // counts) and appends them to `ops`.
   constexpr int TB_RAW = 4096;
   __shared__ unsigned rawl[TB_RAW];
   int nw = 0;
@@ -179,7 +214,9 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
       const unsigned w = (b0 + lane < nw) ? rawl[b0 + lane] : 0u;
       const int k = (int)(w >> 28);
       int c = 0;
-      for (int q = 0; q < k; ++q) c += ((w >> (4 * q)) & 15u) != 0u;
+      if (k == 15) c = (int)(w & 0xffffu);
+      else
+        for (int q = 0; q < k; ++q) c += ((w >> (4 * q)) & 15u) != 0u;
       int incl = c;  // inclusive prefix sum over the lanes
 #pragma unroll
       for (int off = 1; off < 64; off <<= 1) {
@@ -187,172 +224,204 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
         if (lane >= off) incl += y;
       }
       long long o = nops + incl - c;
-      for (int q = 0; q < k; ++q) {
-        const unsigned dl = (w >> (4 * q)) & 15u;
-        if (dl != 0u) {
-          if (o < cap) ops[o] = dl == 9u ? 'M' : (dl == 1u ? 'D' : 'I');
-          ++o;
+      if (k == 15) {
+        for (int q = 0; q < c; ++q, ++o)
+          if (o < cap) ops[o] = 'M';
+      } else {
+        for (int q = 0; q < k; ++q) {
+          const unsigned dl = (w >> (4 * (k - 1 - q))) & 15u;  // step 0 in the top nibble
+          if (dl != 0u) {
+            if (o < cap) ops[o] = dl == 9u ? 'M' : (dl == 1u ? 'D' : 'I');
+            ++o;
+          }
         }
       }
       nops += __shfl(incl, 63);
     }
     nw = 0;
   };
-  auto key_of = [](int s, int g) { return ((long long)s << 32) | (unsigned)g; };
-  // issue the 4 block loads of group (s, g) into stage[cb ^ 1] (blocks past the stripe's
-  // pmax are not loaded, so no read leaves the pair's direction bytes)
-  auto issue_group = [&](int s, int g) {
-    const long long blk0 = (long long)s * pmax + 4ll * g;
-    const unsigned dst = stage_lds + 4096u * (unsigned)(cb ^ 1);
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (4 * g + q < pmax) glds16(base + (blk0 + q) * 1024, dst + 1024u * q);
+  auto record = [&](unsigned w) __attribute__((always_inline)) {
+    rawl[nw] = w;  // every lane stores the same word
+    if (++nw == TB_RAW) decode();
   };
-  int n_switch = 0, n_sync = 0;               // group switches, of them fetched on demand
+  // slot bookkeeping (slot = stripe & 3): the stripe staged there, its first block, and the
+  // count of loads issued up to its own (its loads are complete once at most `issued - end`
+  // later loads are outstanding)
+  int slot_s0 = -1, slot_s1 = -1, slot_s2 = -1, slot_s3 = -1;
+  int slot_b0 = 0, slot_b1 = 0, slot_b2 = 0, slot_b3 = 0;
+  int slot_e0 = 0, slot_e1 = 0, slot_e2 = 0, slot_e3 = 0;
+  int issued = 0;
+  auto sel4 = [](int k, int a, int b, int c, int d) __attribute__((always_inline)) {
+    return k == 0 ? a : (k == 1 ? b : (k == 2 ? c : d));
+  };
+  auto set4 = [](int k, int v, int& a, int& b, int& c, int& d) __attribute__((always_inline)) {
+    a = k == 0 ? v : a;
+    b = k == 1 ? v : b;
+    c = k == 2 ? v : c;
+    d = k == 3 ? v : d;
+  };
+  // the group of stripe s ending a little right of step t (blocks b0 .. b0 + 15 of the stripe)
+  auto group_b0 = [&](int t) __attribute__((always_inline)) {
+    int b0 = ((t + 16) >> 4) - (GB - 1);
+    b0 = b0 < pmax - GB ? b0 : pmax - GB;
+    return b0 > 0 ? b0 : 0;
+  };
+  // stage stripe s, blocks b0.. into slot s & 3 (always 16 loads: a stripe with fewer blocks
+  // loads its last one again, so the outstanding-load arithmetic stays exact)
+  auto stage_group = [&](int s, int b0) __attribute__((always_inline)) {
+    const int k = s & (NSLOT - 1);
+    const unsigned dst = stage_lds + (unsigned)GBYTES * (unsigned)k;
+    const uint8_t* g = base + ((long long)s * pmax + b0) * 1024;
+    if (pmax >= GB) {
+      glds16x16(g, dst);
+    } else {
+#pragma unroll
+      for (int q = 0; q < GB; ++q) glds16(base + ((long long)s * pmax + (q < pmax ? q : pmax - 1)) * 1024, dst + 1024u * q);
+    }
+    issued += GB;
+    set4(k, s, slot_s0, slot_s1, slot_s2, slot_s3);
+    set4(k, b0, slot_b0, slot_b1, slot_b2, slot_b3);
+    set4(k, issued, slot_e0, slot_e1, slot_e2, slot_e3);
+  };
+  int n_switch = 0, n_sync = 0;  // groups staged for the walk, of them on demand
 #ifdef MSA_TB_STATS
-  long long n_outer = 0, n_win = 0, t_win = 0;  // diagnostic build: outer iterations, windows, ticks in windows
+  long long n_run = 0, n_win = 0, t_win = 0;  // diagnostic build: runs, windows, ticks inside groups
 #endif
   long long t_wait = 0;  // diagnostic build: clock ticks spent waiting for group loads
   const long long t_begin = (long long)__builtin_amdgcn_s_memtime();
-  auto timed_wait = [&]() {
-#ifdef MSA_TB_STATS
-    const long long a = (long long)__builtin_amdgcn_s_memtime();
-    vm_wait_all();
-    t_wait += (long long)__builtin_amdgcn_s_memtime() - a;
-#else
-    vm_wait_all();
-#endif
-  };
+  // Windows.  One LDS read gives lane (a, b) = (lane >> 3, lane & 7) the direction byte of
+  // cell (i - a, j - b) -- (r - a, tg - a - b) in the group -- and the lane turns it into its
+  // transition word (tb_word).  A step is then a v_readlane of the word at the walk's lane
+  // index plus a few scalar ops; seven steps stay inside the 8 x 8 window.  A lane whose cell
+  // lies outside the group or on the matrix border (i - a < 1 or j - b < 1) holds the FROZEN
+  // word instead (every state: lane step 0, stay), so a window needs no step budget: a walk
+  // that reaches such a cell stops there, and the next group takes over.
+  // The byte of (rr, tt) sits at ((tt >> 4) << 10) | (rr << 4) | (tt & 15) of the group.
+  // With u = tg & 15 and d = u - (a + b) in [-14, 15]: tt >> 4 = (tg >> 4) + (d >> 4) and
+  // tt & 15 = d & 15, so the address is a uniform part plus d + 1008 (d >> 4) - 16a.
+  const int wa = lane >> 3, wb = lane & 7;
+  const int wc = wa + wb, wa16 = 16 * wa;
+  constexpr unsigned FROZEN = (10u << 10) | (20u << 20) | (1u << 31);
   if (REF || r0.score > 0) {
     bool stopped = false;
-    // outer iteration: make the group under (i, j) current, keep the next one in flight,
-    // then run the steps that provably stay inside the group without any further checks
+    int s_cur = -1, cs = 0;
+    // outer iteration: the walk entered a stripe, or left its group on the left
     while (i > 0 && j > 0 && !stopped) {
       const int s = (i - 1) >> 6;
       int r = (i - 1) & 63;
-      if (s != s_cached) {
+      const bool entered = s != s_cur;
+      if (entered) {
         cs = cs_of(s);
-        cs_up = s > 0 ? cs_of(s - 1) : 0;
-        s_cached = s;
+        s_cur = s;
       }
-      int t = j - cs + r;
-      const int g = t >> 6;
-      const long long key = key_of(s, g);
-      if (key != cur_key) {
-        ++n_switch;
-        if (pend) {
-          timed_wait();
-          pend = false;
-          if (key != nxt_key) issue_group(s, g), timed_wait(), ++n_sync;  // mispredicted: fetch now
-        } else {
-          issue_group(s, g);
-          timed_wait();
-          ++n_sync;
-        }
-        nxt_key = -1;
-        cb ^= 1;  // the fetched group becomes current
-        cur_key = key;
+      const int t = j - cs + r;
+      const int k = s & (NSLOT - 1);
+      int b0 = sel4(k, slot_b0, slot_b1, slot_b2, slot_b3);
+      if (!entered || sel4(k, slot_s0, slot_s1, slot_s2, slot_s3) != s || t < 16 * b0 || t >= 16 * b0 + GT) {
+        // not staged (the first stripe, a misprediction, or a walk that left the group on
+        // the left): stage it now
+        b0 = group_b0(t);
+        stage_group(s, b0);
+        ++n_sync;
       }
-      // steps that stay in this group (each lowers r by <= 1 and t by <= 2) and inside the
-      // matrix (i and j drop by <= 1 per step)
-      const int to_top = r + 1, to_left = ((t & 63) >> 1) + 1;
-      int budget = to_top < to_left ? to_top : to_left;
-      budget = budget < i ? budget : i;
-      budget = budget < j ? budget : j;
-      // prefetch the group the walk leaves into: the stripe above (at the column a
-      // diagonal path exits through) if the top row comes first, else the group to the left
-      long long want = -1;
-      int ws = 0, wg = 0;
-      if (to_top <= to_left) {
-        const int tu = (j - r) - cs_up + 63;
-        if (s > 0 && tu >= 0) {
-          ws = s - 1;
-          wg = tu >> 6;
-          want = key_of(ws, wg);
-        }
-      } else if (g > 0) {
-        ws = s;
-        wg = g - 1;
-        want = key_of(ws, wg);
-      }
-      if (want >= 0 && want != nxt_key && want != cur_key) {
-        if (pend) timed_wait();  // stage[cb ^ 1] is about to be refilled
-        issue_group(ws, wg);
-        nxt_key = want;
-        pend = true;
-      }
-      const int r_in = r, t_in = t;
-      // The budget's steps run in windows of up to 7.  One LDS read gives lane (a, b) =
-      // (lane >> 3, lane & 7) the direction byte of cell (i - a, j - b) -- (r - a, t - a - b) in
-      // the group -- and the lane turns it into its transition word (tb_word).  A step is then
-      // a v_readlane of the word at the walk's lane index plus a few scalar ops; seven steps
-      // stay inside the 8 x 8 window, the budget keeps them inside the group.
-      // The byte of (rr, tt) sits at ((tt >> 4) << 10) | (rr << 4) | (tt & 15) of the group.
-      // With u = t & 15 and d = u - (a + b) in [-14, 15]: tt >> 4 = (t >> 4) + (d >> 4) and
-      // tt & 15 = d & 15, so the address is a uniform part plus d + 1008 (d >> 4) - 16a (lanes
-      // outside the group land in the guard or an unused byte, never reached).
-      const unsigned grp_lds = stage_lds + 4096u * (unsigned)cb;
-      const int wc = (lane >> 3) + (lane & 7), wa16 = 16 * (lane >> 3);
-      bool stop = false;
+      ++n_switch;
+      {
 #ifdef MSA_TB_STATS
-      ++n_outer;
+        const long long a = (long long)__builtin_amdgcn_s_memtime();
+#endif
+        vm_wait_le(issued - sel4(k, slot_e0, slot_e1, slot_e2, slot_e3));
+#ifdef MSA_TB_STATS
+        t_wait += (long long)__builtin_amdgcn_s_memtime() - a;
+#endif
+      }
+      if (entered) {
+        // prefetch the next three stripes' groups (only s - 3 is new in steady state): a
+        // diagonal path from (i, j) enters stripe s - d at column j - r - 64d + 63, step
+        // t_d = j - r - 64d + 126 - cs(s - d); the group ends 16 steps right of it
+        for (int d = 1; d <= NSLOT - 1; ++d) {
+          const int sd = s - d;
+          if (sd < 0) break;
+          if (sel4(sd & (NSLOT - 1), slot_s0, slot_s1, slot_s2, slot_s3) == sd) continue;
+          stage_group(sd, group_b0(j - r - 64 * d + 126 - cs_of(sd)));
+        }
+      }
+      const unsigned grp_lds = stage_lds + (unsigned)GBYTES * (unsigned)k;
+      int tg = t - 16 * b0;
+#ifdef MSA_TB_STATS
       const long long tw0 = (long long)__builtin_amdgcn_s_memtime();
 #endif
-      int sh = 9 * st;
-      while (budget > 0 && !stop) {
-        const int kmax = budget < 7 ? budget : 7;
-        const int tg = t & 63;
-        const int d = (tg & 15) - wc;
-        const unsigned ga = grp_lds + (unsigned)(((tg >> 4) << 10) + (r << 4)) + (unsigned)(d + 1008 * (d >> 4) - wa16);
-        const unsigned dv = *(const lds_u8*)(uintptr_t)ga;
-        const int wt = (int)tb_word<KIND>(dv);
-        int idx = 0, k = 0;
-        unsigned wcode = 0;
-        if (kmax == 7) {
-          // a full window (the common case), unrolled and branch-free: per step a v_readlane,
-          // a 64-bit shift (the absorbing stop, tb_word) and five scalar ops
-#pragma unroll
-          for (int kk = 0; kk < 7; ++kk) {
-            const unsigned long long w64 = (13ull << 32) | (unsigned)__builtin_amdgcn_readlane(wt, idx);
-            const unsigned f = (unsigned)(w64 >> sh);
-            const unsigned dl = f & 15u;
-            sh = (int)((f >> 4) & 31u);
-            idx += (int)dl;
-            wcode |= dl << (4 * kk);
-          }
-          k = 7;
-        } else {
-          for (; k < kmax; ++k) {
-            const unsigned long long w64 = (13ull << 32) | (unsigned)__builtin_amdgcn_readlane(wt, idx);
-            const unsigned f = (unsigned)(w64 >> sh);
-            const unsigned dl = f & 15u;
-            sh = (int)((f >> 4) & 31u);
-            idx += (int)dl;
-            wcode |= dl << (4 * k);
+      int sh = 10 * st;
+      for (;;) {
+        if (sh == 0) {
+          // diagonal run: lane q reads cell (i - q, j - q) (inside the group and the matrix
+          // for q <= qmax); the run is the number of leading lanes that continue diagonally
+          // in state 0, the walk moves that many cells at once
+          int qmax = r < (tg >> 1) ? r : (tg >> 1);
+          qmax = qmax < i - 1 ? qmax : i - 1;
+          qmax = qmax < j - 1 ? qmax : j - 1;
+          const bool valid = lane <= qmax;
+          const int tt = tg - 2 * lane, rr = r - lane;
+          const unsigned ga = grp_lds + (valid ? (unsigned)(((tt >> 4) << 10) + (rr << 4) + (tt & 15)) : 0u);
+          const unsigned dv = *(const lds_u8*)(uintptr_t)ga;
+          const unsigned long long bal = __ballot(valid && tb_diag_stay<KIND>(dv));
+          const int q = ~bal == 0ull ? 64 : (int)__builtin_ctzll(~bal);  // leading "diagonal, stay" cells
+#ifdef MSA_TB_STATS
+          ++n_run;
+#endif
+          if (q > 0) {
+            record((15u << 28) | (unsigned)q);
+            r -= q;
+            tg -= 2 * q;
+            i -= q;
+            j -= q;
+            if (r < 0 || tg < 0 || i <= 0 || j <= 0) break;
           }
         }
-        stop = sh == 27;  // the steps after a stop recorded no-op nibbles
-        rawl[nw] = wcode | ((unsigned)k << 28);  // every lane stores the same word
-        if (++nw == TB_RAW) decode();
+        // a window of seven steps
+        int wt;
+        {
+          const int d = (tg & 15) - wc;
+          const unsigned ga = grp_lds + (unsigned)(((tg >> 4) << 10) + (r << 4)) + (unsigned)(d + 1008 * (d >> 4) - wa16);
+          const unsigned dv = *(const lds_u8*)(uintptr_t)ga;
+          const bool live = wa <= min(r, i - 1) && wb <= j - 1 && wc <= tg;
+          const unsigned w = tb_word<KIND>(dv);  // (evaluated for every lane: a select, no branch)
+          wt = (int)(live ? w : FROZEN);
+        }
+        int idx = 0;
+        unsigned wcode = 0;
+        // seven steps, unrolled and branch-free: per step a v_readlane, a 64-bit shift (the
+        // absorbing stop, tb_word), a bit-field extract, an add and the record
+#pragma unroll
+        for (int kk = 0; kk < 7; ++kk) {
+          const unsigned long long w64 = (7ull << 32) | (unsigned)__builtin_amdgcn_readlane(wt, idx);
+          const unsigned f = (unsigned)(w64 >> (sh & 63));
+          const unsigned dl = (f >> 6) & 15u;
+          sh = (int)f;
+          idx += (int)dl;
+          wcode = (wcode << 4) + dl;
+        }
+        sh &= 31;
+        record(wcode | (7u << 28));
         const int da = idx >> 3, db = idx & 7;
         r -= da;
-        t -= da + db;
-        budget -= k;
+        tg -= da + db;
+        i -= da;
+        j -= db;
 #ifdef MSA_TB_STATS
         ++n_win;
 #endif
+        // stop; or the walk left the group (top row or left edge) or reached the border
+        if (sh == 30 || r < 0 || tg < 0 || i <= 0 || j <= 0) break;
       }
 #ifdef MSA_TB_STATS
       t_win += (long long)__builtin_amdgcn_s_memtime() - tw0;
 #endif
-      st = stop ? 3 : sh / 9;
-      i -= r_in - r;                  // rows consumed
-      j -= (t_in - t) - (r_in - r);   // columns consumed
+      st = (sh == 30) ? 3 : sh / 10;
       if constexpr (REF) {
         // a cell without a predecessor table (cannot happen for a complete fill)
         if (st == 3) { status = -9; stopped = true; }  // MSA_ERR_NOMATCH
-        // find_alignment stops at the matrix border (:147); the budget (<= min(i, j)) makes
-        // a window end exactly there
+        // find_alignment stops at the matrix border (:147): the border cells' frozen words end
+        // the walk exactly there
       } else if (st == 3) {  // local start (H came from 0): the walk ends at this cell
         st = 0;
         stopped = true;
@@ -361,7 +430,7 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
   }
   decode();  // the words still in the ring
   if (nops > cap && status == 0) status = -8;  // MSA_ERR_CAPACITY
-  if (pend) vm_wait_all();  // no load left in flight when the wave ends
+  vm_wait_all();  // no load left in flight when the wave ends
   if (lane == 0) {
     info[0] = nops;
     info[1] = i + 1;
@@ -370,7 +439,7 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
     info[4] = n_switch;
     info[5] = n_sync;
 #ifdef MSA_TB_STATS
-    info[3] = n_outer;
+    info[3] = n_run;
     info[5] = n_win;
     info[7] = t_win;
 #endif
