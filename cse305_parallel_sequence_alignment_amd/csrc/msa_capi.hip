@@ -305,8 +305,9 @@ kfn_t pick_kernel(int alg, int out, int tp, bool sgl) {
 
 // single-pair SW linear (msa_flow.hip): pass 1 (chain), pass 2 (fill + H)
 kfn_t pick_flow(int alg, bool best, bool save, int tp, int R) {
-  // SW affine (direction bytes): pass 1 + in-launch pass 2, one row per lane
-  if (alg == MSA_ALG_SWA) return (save && R == 1) ? flow_kernel<true, false, true, true, 1, true> : nullptr;
+  // SW affine / the reference's Gotoh (direction bytes): pass 1 + in-launch pass 2, one row per lane
+  if (alg == MSA_ALG_SWA) return (save && R == 1) ? flow_kernel<true, false, true, true, 1, 1> : nullptr;
+  if (alg == MSA_ALG_REF1) return (save && R == 1) ? flow_kernel<true, false, true, true, 1, 2> : nullptr;
   // score-only plans: pass 1 alone, one row per lane, best cell tracked in the chain;
   // H plans: pass 1 + in-launch pass 2, two rows per lane
   const bool fl = (alg == MSA_ALG_SWL);
@@ -509,19 +510,23 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   const bool single = desc->single != 0;
   P->d.single = single ? 1 : 0;
   // flow kernels: one SW-linear pair whose 8 LDS code copies fit next to the rings
-  // (n <= ~19.5k columns), or one SW-affine pair with direction bytes (two values per link
-  // column, 4 code copies: n <= ~37k); wider pairs run the one-pass stripe kernel
-  const bool aff = kalg == MSA_ALG_SWA;
+  // (n <= ~19.5k columns), or one SW-affine / reference-Gotoh (start type -1, tagged) pair
+  // with direction bytes (two values per link column, 4 code copies: n <= ~37k); wider pairs
+  // run the one-pass stripe kernel
+  const bool aff = kalg == MSA_ALG_SWA || kalg == MSA_ALG_REF1;
   const size_t flow_lds = (size_t)(FL_FLAGS + (FL_W + 1) * 256 * (aff ? 2 : 1)) * 4 +
                           (size_t)(aff ? 4 : FL_NCOPY) * fl_code_bytes((int)desc->n[0]);
   // affine: profile bytes score + 2e + (o - e) must be int8
-  const bool aff_ok = aff && out_mode == MSA_OUT_DIR && desc->gap_extend >= 0 &&
+  const bool aff_ok = kalg == MSA_ALG_SWA && out_mode == MSA_OUT_DIR && desc->gap_extend >= 0 &&
                       desc->gap_open >= desc->gap_extend &&
                       std::max(desc->match, desc->mismatch) + desc->gap_open + desc->gap_extend <= 127 &&
                       std::min(desc->match, desc->mismatch) + desc->gap_open + desc->gap_extend >= -128 &&
                       (int64_t)desc->gap_extend * (desc->m[0] + desc->n[0] + 2) < (int64_t(1) << 28);
+  // Gotoh: profile bytes 4 (f + 2g) <= 127; the shifted tagged values 4 (T + g(i+j)) stay far
+  // inside int32 (REF1's own bound covers the shift: |T| + g(i+j) <= (g+h+1) span)
+  const bool got_ok = kalg == MSA_ALG_REF1 && out_mode == MSA_OUT_DIR && 4 * (1 + 2 * desc->gap_extend) <= 127;
   const bool flow = single && ((kalg == MSA_ALG_SWL || kalg == MSA_ALG_SWL0) ?
-                               (out_mode == MSA_OUT_H || (out_mode == MSA_OUT_NONE && !tp)) : aff_ok) &&
+                               (out_mode == MSA_OUT_H || (out_mode == MSA_OUT_NONE && !tp)) : (aff_ok || got_ok)) &&
                     desc->m[0] > 0 && flow_lds <= 160 * 1024;
   P->flow = flow;
   P->flow2 = flow && (out_mode == MSA_OUT_H || aff);
@@ -790,8 +795,9 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     }
     std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return key[x] < key[y]; });
     // (affine: the F~ bottom rows follow the Z rows; a snapshot is 4 values per lane)
-    const size_t brb = sizeof(unsigned long long) * (size_t)S * P->brw * (P->kp.alg == MSA_ALG_SWA ? 2 : 1);
-    const size_t snb = sizeof(unsigned long long) * (size_t)P->nblk * (P->kp.alg == MSA_ALG_SWA ? 256 : 128 * P->R);
+    const bool two = P->kp.alg == MSA_ALG_SWA || P->kp.alg == MSA_ALG_REF1;
+    const size_t brb = sizeof(unsigned long long) * (size_t)S * P->brw * (two ? 2 : 1);
+    const size_t snb = sizeof(unsigned long long) * (size_t)P->nblk * (two ? 256 : 128 * P->R);
     if (!P->alloc(&P->d_br, brb) || hipMemset(P->d_br, 0, brb) != hipSuccess) return fail();
     if (!P->alloc(&P->d_snap, snb) || hipMemset(P->d_snap, 0, snb) != hipSuccess) return fail();
     if (!P->alloc(&P->d_blk, sizeof(int4) * (size_t)P->nblk)) return fail();
@@ -918,7 +924,7 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
     HIPCHK(hipGetLastError());
   }
   if (ev) HIPCHK(hipEventRecord(P->ev1, st));
-  if (P->flow2) {
+  if (P->flow2 && P->kp.alg != MSA_ALG_REF1) {  // (Gotoh: the final state is in the last stripe's meta)
     hipLaunchKernelGGL(reduce_blocks_kernel, dim3(1), dim3(1024), 0, st, (const int4*)P->d_blk, P->nblk, P->d_res);
     HIPCHK(hipGetLastError());
     return MSA_OK;

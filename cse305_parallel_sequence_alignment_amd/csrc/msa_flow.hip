@@ -211,6 +211,19 @@ __device__ __forceinline__ void fl_profile_aff(int match, int mismatch, int e, i
   phi = hi & 0x00ffffffu;
 }
 
+// Gotoh profile (tagged, shifted): 4 (f + 2g), f = 1 on a match, 0 otherwise (the reference's
+// f, main_alignment.cpp); the virtual code 7 (columns past n) gets 0.
+__device__ __forceinline__ void fl_profile_got(int g, unsigned ac, unsigned& plo, unsigned& phi) {
+  const int sm = 4 * (1 + 2 * g), sx = 8 * g;
+  const unsigned bx = (unsigned)(sx & 0xff) * 0x01010101u;
+  unsigned lo = bx, hi = bx;
+  const unsigned bm = (unsigned)(sm & 0xff);
+  if (ac < 4) lo = (lo & ~(0xffu << (8 * ac))) | (bm << (8 * ac));
+  else hi = (hi & ~(0xffu << (8 * (ac - 4)))) | (bm << (8 * (ac - 4)));
+  plo = lo;
+  phi = hi & 0x00ffffffu;
+}
+
 // Substitution profile of a row: score + g (X-space) or + 2g (G-space) for
 // codes 0..7; code 7 = virtual column (outside [1, n]): score 0 without the
 // floor (keeps H = 0 left of column 1, never above a real cell right of n),
@@ -255,6 +268,17 @@ __device__ __forceinline__ int fl_step(int in, int s, int& X, int& U, int g) {
 // carry both (two values per column in the rings, granules and bottom rows), a lane's state
 // is (Z left, E~, F~, diagonal Z).  The direction byte is stripe_kernel's MSA_ALG_SWA byte:
 // every tie test compares values at one cell, which the shift leaves exact.
+// GOT: the reference's Gotoh recurrence, start type -1, in stripe_kernel's tagged form
+// (MSA_ALG_REF1: value x 4 + tag, max() = the reference's first-maximum table order) and
+// shifted by g(i+j) as above:
+//   t1 = (H~diag | 3) + 4(f + 2g),  t2 = (R~left & ~3) | 2,  t3 = (D~up & ~3) | 1
+//   H~ = max(t1, t2, t3),  R~ = max(t1 - 4h, t2, t3 - 4h),  D~ = max(t1 - 4h, t2 - 4h, t3)
+// (R~ / D~ = T2 of the cell to the right / T3 of the cell below; the gap extension g is
+// absorbed by the shift, so the borders are constants: row 0 (3, 3 - 4h) at column 0 and
+// (2 - 4h, 2 - 8h) right of it, column 0 (1 - 4h, 1 - 8h, 1 - 4h)).  Links carry H~ and D~,
+// a lane's state is (H~, R~, D~, diagonal H~); the first 6 phases hold lanes still left of
+// column 1 at the column-0 border (stripe_kernel's LB masking).  Pass 2 writes the tag bytes
+// traceback_kernel<TB_REF_TAG> walks and the (m, n) tables find_alignment's end rule reads.
 // What a pass-2 block needs, by value (a reference to the kernel's KArgs would
 // put them on the stack of the pass-1 path too).
 struct FillArgs {
@@ -268,16 +292,21 @@ struct FillArgs {
   long long cod_copy, a_off, cod_off, out_off;
   int m, n, pmax, nseg, brw, match, mismatch, g;
   unsigned ep;
-  uint8_t* outDir;  // affine: direction bytes
-  int oe;           // affine: gap_open - gap_extend (g = gap_extend)
+  uint8_t* outDir;  // affine / Gotoh: direction bytes
+  int oe;           // affine: gap_open - gap_extend (g = gap_extend); Gotoh: h
+  msa_stripe_meta* meta;  // Gotoh: the final cell's tables go to the last stripe's meta
+  int stripe0;
 };
 template <bool FLOOR, bool TRACKPOS, int R>
 __device__ __attribute__((noinline)) void fill_block(const FillArgs f, int blk, int lane, int* lds);
 __device__ __attribute__((noinline)) void fill_block_aff(const FillArgs f, int blk, int lane, int* lds);
+__device__ __attribute__((noinline)) void fill_block_got(const FillArgs f, int blk, int lane, int* lds);
 
-template <bool FLOOR, bool BEST, bool SAVE, bool TRACKPOS, int R = 1, bool AFF = false>
+template <bool FLOOR, bool BEST, bool SAVE, bool TRACKPOS, int R = 1, int FK = 0>
 __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
   constexpr bool GS = !FLOOR;
+  constexpr bool AFF = FK != 0;  // two values per link column (affine SW, Gotoh)
+  constexpr bool GOT = FK == 2;  // the reference's Gotoh, tagged
   static_assert(R == 1 || (R == 2 && !BEST), "two rows per lane: pass-2 plans only");
   static_assert(!AFF || (R == 1 && SAVE && !BEST), "affine: two-pass, one row per lane");
   constexpr int NV = AFF ? 2 : 1;                  // values per column on a link (Z, F~)
@@ -322,8 +351,9 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         const FillArgs f{a.A, a.cod, a.br, a.snap, a.outH, a.blk, a.err, a.cod_copy, a.pairs[0].a_off,
                          a.pairs[0].cod_off, a.pairs[0].out_off, a.pairs[0].m, a.pairs[0].n, a.pairs[0].pmax,
                          a.nseg, a.brw, kp.match, kp.mismatch, kp.gap_ext, kp.epoch, a.outDir,
-                         kp.gap_open - kp.gap_ext};
-        if constexpr (AFF) fill_block_aff(f, a.border[t], lane, smem + w * 544);
+                         kp.gap_open - kp.gap_ext, a.meta, a.pairs[0].stripe0};
+        if constexpr (GOT) fill_block_got(f, a.border[t], lane, smem + w * 544);
+        else if constexpr (AFF) fill_block_aff(f, a.border[t], lane, smem + w * 544);
         else fill_block<FLOOR, TRACKPOS, R>(f, a.border[t], lane, smem + w * 544);
       }
       return;
@@ -398,6 +428,10 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
             const int col = cs_c + 16 * b + 64 * r + lane;
             val[r] = AFF ? g * col - oe : (GS ? g * col : -g);  // row 0: H = 0 (affine: Z; F~ = -inf)
             valf[r] = MSA_NEG;
+            if constexpr (GOT) {  // row 0, tagged and shifted (oe = h)
+              val[r] = col < 0 ? MSA_NEG : (col == 0 ? 3 : 2 - 4 * oe);
+              valf[r] = col < 0 ? MSA_NEG : (col == 0 ? 3 - 4 * oe : 2 - 8 * oe);
+            }
           }
           nb = min(16, Bmax - b + 1);
         } else {
@@ -523,7 +557,8 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
       const unsigned a_cons1 = lds_addr(w + 1 < W ? flags + 32 + w + 2 : flags + 64 + W);
       const unsigned a_cons2 = lds_addr(flags + 64 + w + 1);
       unsigned plo, phi;
-      fl_profile_aff(kp.match, kp.mismatch, g, oe, ac, plo, phi);
+      if constexpr (GOT) fl_profile_got(g, ac, plo, phi);
+      else fl_profile_aff(kp.match, kp.mismatch, g, oe, ac, plo, phi);
       unsigned a_code;
       {
         const int c0 = cs - lane + FL_OFF;
@@ -531,10 +566,18 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         a_code = lds_addr(reinterpret_cast<int*>(codes + x * L8 + (c0 - x)));
       }
       // step 0: lane r at column cs - r (virtual, H = 0): its left cell's Z, the diagonal Z
+      // (Gotoh: Zl / E / Fo / U hold H~ / R~ / D~ / diagonal H~, the column-0 border)
       const int flr0 = g * (64 * k + 1 + cs);  // e(i+j) at step 0, every lane
       int Zl = g * (row_i + cs - lane - 1) - oe;
       int U = Zl - g;
       int E = MSA_NEG, Fo = MSA_NEG;
+      const int tmin = 1 - cs + lane;  // Gotoh: the lane's first step at column >= 1
+      if constexpr (GOT) {
+        Zl = 1 - 4 * oe;
+        E = 1 - 8 * oe;
+        Fo = 1 - 4 * oe;
+        U = MSA_NEG;
+      }
       int pubv = 0, consv = 0;
       unsigned spins = 0;
       fl_v4i ZA[4], FA[4], ZB[4], FB[4];
@@ -600,8 +643,10 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         mask_in(0, ZA, FA);
       }
       auto run_phase = [&](const int q, fl_v4i (&Z)[4], fl_v4i (&F)[4], fl_v2u& Cl, fl_v2u& Ch, fl_v4i (&Zn)[4],
-                           fl_v4i (&Fn)[4], fl_v2u& Cln, fl_v2u& Chn, auto MASK_) __attribute__((always_inline)) {
+                           fl_v4i (&Fn)[4], fl_v2u& Cln, fl_v2u& Chn, auto MASK_, auto HEAD_)
+          __attribute__((always_inline)) {
         constexpr bool MASK = decltype(MASK_)::value;
+        constexpr bool HEAD = decltype(HEAD_)::value;  // Gotoh: lanes left of column 1 hold the border
         const int need = MASK ? min(q + 1, Bin + 1) : q + 1;
         if (pubv - dq_in < need) {
 #ifdef MSA_STAMPS
@@ -632,6 +677,30 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
             const int kx = 4 * u + kk;
             if (kx == FL_PF) issue_reads(q + 1, Zn, Fn, Cln, Chn, pubn);
             const int sc = ((int)(s4 << (24 - 8 * kk))) >> 24;
+            if constexpr (GOT) {
+              const int uH = dpp_shr1(Z[kx >> 2][kx & 3], Zl);
+              const int uD = dpp_shr1(F[kx >> 2][kx & 3], Fo);
+              const int t1 = (int)((unsigned)U | 3u) + sc;
+              const int t2 = (int)(((unsigned)E & ~3u) | 2u);
+              const int t3 = (int)(((unsigned)uD & ~3u) | 1u);
+              const int t1h = t1 - 4 * oe;
+              int h = imax3(t1, t2, t3);
+              int rr = imax3(t1h, t2, t3 - 4 * oe);
+              int dd = imax3(t1h, t2 - 4 * oe, t3);
+              asm("" : "+v"(h));
+              if constexpr (HEAD) {
+                const bool before = 16 * q + kx < tmin;
+                h = before ? 1 - 4 * oe : h;
+                rr = before ? 1 - 8 * oe : rr;
+                dd = before ? 1 - 4 * oe : dd;
+              }
+              U = uH;
+              Zl = h;
+              E = rr;
+              Fo = dd;
+              xz[kx] = h;
+              xf[kx] = dd;
+            } else {
             const int upZ = dpp_shr1(Z[kx >> 2][kx & 3], Zl);
             const int upF = dpp_shr1(F[kx >> 2][kx & 3], Fo);
             const int e = imax(E, Zl);
@@ -645,6 +714,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
             Zl = h - oe;
             xz[kx] = Zl;
             xf[kx] = f;
+            }
           }
         }
         lgkm_wait<10>(pubn);  // the counter read (oldest of the eleven) has landed
@@ -668,24 +738,43 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
       using F_ = std::false_type;
       const int qa = max(0, min(P, Bin));
       int q = 0;
+      bool done = false;
+      if constexpr (GOT) {
+        // head: phases 0..5 (steps < 96 > every lane's tmin <= 79) hold the column-0 border
+        if (qa >= 6) {
+          for (; q < 6; q += 2) {
+            run_phase(q, ZA, FA, CAl, CAh, ZB, FB, CBl, CBh, F_{}, T_{});
+            run_phase(q + 1, ZB, FB, CBl, CBh, ZA, FA, CAl, CAh, F_{}, T_{});
+          }
+        } else {  // a short stripe: every phase masked both ways
+          for (; q + 1 < P; q += 2) {
+            run_phase(q, ZA, FA, CAl, CAh, ZB, FB, CBl, CBh, T_{}, T_{});
+            run_phase(q + 1, ZB, FB, CBl, CBh, ZA, FA, CAl, CAh, T_{}, T_{});
+          }
+          if (q < P) run_phase(q, ZA, FA, CAl, CAh, ZB, FB, CBl, CBh, T_{}, T_{});
+          done = true;
+        }
+      }
+      if (!done) {
       for (; q + 1 < qa; q += 2) {
-        run_phase(q, ZA, FA, CAl, CAh, ZB, FB, CBl, CBh, F_{});
-        run_phase(q + 1, ZB, FB, CBl, CBh, ZA, FA, CAl, CAh, F_{});
+        run_phase(q, ZA, FA, CAl, CAh, ZB, FB, CBl, CBh, F_{}, F_{});
+        run_phase(q + 1, ZB, FB, CBl, CBh, ZA, FA, CAl, CAh, F_{}, F_{});
       }
       if (q < qa) {
-        run_phase(q, ZA, FA, CAl, CAh, ZB, FB, CBl, CBh, F_{});
+        run_phase(q, ZA, FA, CAl, CAh, ZB, FB, CBl, CBh, F_{}, F_{});
         ++q;
         for (; q + 1 < P; q += 2) {
-          run_phase(q, ZB, FB, CBl, CBh, ZA, FA, CAl, CAh, T_{});
-          run_phase(q + 1, ZA, FA, CAl, CAh, ZB, FB, CBl, CBh, T_{});
+          run_phase(q, ZB, FB, CBl, CBh, ZA, FA, CAl, CAh, T_{}, F_{});
+          run_phase(q + 1, ZA, FA, CAl, CAh, ZB, FB, CBl, CBh, T_{}, F_{});
         }
-        if (q < P) run_phase(q, ZB, FB, CBl, CBh, ZA, FA, CAl, CAh, T_{});
+        if (q < P) run_phase(q, ZB, FB, CBl, CBh, ZA, FA, CAl, CAh, T_{}, F_{});
       } else {
         for (; q + 1 < P; q += 2) {
-          run_phase(q, ZA, FA, CAl, CAh, ZB, FB, CBl, CBh, T_{});
-          run_phase(q + 1, ZB, FB, CBl, CBh, ZA, FA, CAl, CAh, T_{});
+          run_phase(q, ZA, FA, CAl, CAh, ZB, FB, CBl, CBh, T_{}, F_{});
+          run_phase(q + 1, ZB, FB, CBl, CBh, ZA, FA, CAl, CAh, T_{}, F_{});
         }
-        if (q < P) run_phase(q, ZA, FA, CAl, CAh, ZB, FB, CBl, CBh, T_{});
+        if (q < P) run_phase(q, ZA, FA, CAl, CAh, ZB, FB, CBl, CBh, T_{}, F_{});
+      }
       }
       lgkm_wait_aff<0>(ZA, FA, CAl, CAh);
       lgkm_wait_aff<0>(ZB, FB, CBl, CBh);
@@ -1258,6 +1347,167 @@ __device__ __attribute__((noinline)) void fill_block_aff(const FillArgs a, int b
     if (ob > bb || (ob == bb && (oi < bi || (oi == bi && oj < bj)))) { bb = ob; bi = oi; bj = oj; }
   }
   if (lane == 0) a.blk[blk] = make_int4(bb, bi, bj, 0);
+}
+
+// Pass 2, Gotoh (the reference's main_alignment_function path): block (stripe s, segment
+// seg) recomputes its FL_PS phases from SNAP (H~, R~, D~, diagonal H~ per lane) and the
+// stripe above's bottom row (H~ and D~ granules) and writes the tag bytes (T1's, T2's, T3's
+// predecessor: the diagonal H~'s, the left R~'s and the upper D~'s tag) in the skewed stripe
+// layout.  The block holding cell (m, n) stores its three tables, unshifted, as the last
+// stripe's final state (reduce_pairs_kernel turns it into the pair result, the walk reads
+// find_alignment's end rule from it).
+__device__ __attribute__((noinline)) void fill_block_got(const FillArgs a, int blk, int lane, int* lds) {
+  const unsigned ep = a.ep;
+  const int m = a.m, n = a.n, S = (m + 63) / 64, g = a.g, h4 = 4 * a.oe;
+  const int s = blk / a.nseg, seg = blk - s * a.nseg;
+  if (s < S) {
+    const int P = fl_P(s, m, n, 1);
+    const int q0 = seg * FL_PS;
+    if (q0 < P) {
+      int q1 = min(P, q0 + FL_PS);
+      const int cs = fl_cs(s);
+      const int row_i = 64 * s + lane + 1;
+      const unsigned ac = (row_i <= m) ? (a.A[a.a_off + row_i - 1] & 7u) : 0u;
+      unsigned plo, phi;
+      fl_profile_got(g, ac, plo, phi);
+      const int Bin = (s == 0) ? P - 1 : min(P - 1, fl_bmax(s, m, n, 1));
+      const unsigned long long* sp = a.snap + ((size_t)s * a.nseg + seg) * 256 + lane;
+      const unsigned long long* brz = a.br + (size_t)(s > 0 ? s - 1 : 0) * a.brw;
+      const unsigned long long* brf = a.br + (size_t)(S + (s > 0 ? s - 1 : 0)) * a.brw;
+      const int qb = (s > 0) ? min(q1, Bin + 1) : q0;
+      const int nv = 16 * max(0, qb - q0);
+      int Hs = 0, Rs = 0, Ds = 0, U = 0;
+      bool ready = (nv == 0);
+      for (int t2 = 0; !ready && t2 < (int)(FL_SPIN_MAX >> 2); ++t2) {
+        const unsigned long long gz = gload(brz + 16 * q0 + nv - 1), gf = gload(brf + 16 * q0 + nv - 1);
+        ready = __ballot((unsigned)(gz >> 32) != ep || (unsigned)(gf >> 32) != ep) == 0;
+        if (!ready) __builtin_amdgcn_s_sleep(FL_FSLEEP);
+      }
+      if (ready) {
+        ready = false;
+        for (int tries = 0; !ready && tries < (int)FL_SPIN_MAX; ++tries) {
+          const unsigned long long x0 = gload(sp), x1 = gload(sp + 64), x2 = gload(sp + 128), x3 = gload(sp + 192);
+          bool ok = ((unsigned)(x0 >> 32) == ep) && ((unsigned)(x1 >> 32) == ep) && ((unsigned)(x2 >> 32) == ep) &&
+                    ((unsigned)(x3 >> 32) == ep);
+          Hs = (int)(unsigned)x0;
+          Rs = (int)(unsigned)x1;
+          Ds = (int)(unsigned)x2;
+          U = (int)(unsigned)x3;
+          for (int v = lane; v < nv; v += 64) {
+            const unsigned long long gz = gload(brz + 16 * q0 + v), gf = gload(brf + 16 * q0 + v);
+            ok = ok && ((unsigned)(gz >> 32) == ep) && ((unsigned)(gf >> 32) == ep);
+            *L(lds + v) = (int)(unsigned)gz;
+            *L(lds + 256 + v) = (int)(unsigned)gf;
+          }
+          ready = __ballot(!ok) == 0;
+          if (!ready) __builtin_amdgcn_s_sleep(8);
+        }
+      }
+      if (!ready) {
+        if (lane == 0) atomicExch(a.err, 15);
+        q1 = q0;
+      }
+      FL_CBAR();
+      const int b0 = cs - lane - 1 + MSA_CPAD;
+      const unsigned* cptr = reinterpret_cast<const unsigned*>(a.cod + (size_t)(b0 & (MSA_NCOPY - 1)) * a.cod_copy +
+                                                             a.cod_off + (b0 & ~(MSA_NCOPY - 1)));
+      const int tmin = 1 - cs + lane;
+      // the final cell (m, n): the lane of row m at step n - cs + lane of the last stripe
+      const int tf = (row_i == m) ? n - cs + lane : -1;
+      fl_v4u* dp = reinterpret_cast<fl_v4u*>(a.outDir + (size_t)a.out_off + (size_t)s * a.pmax * 1024) + lane;
+      auto ldc = [&](int q) __attribute__((always_inline)) {
+        return *reinterpret_cast<const uint4*>(cptr + 4 * min(q, P - 1));
+      };
+      uint4 cr0 = ldc(q0), cr1 = ldc(q0 + 1), cr2 = ldc(q0 + 2), cr3 = ldc(q0 + 3);
+      auto phase = [&](const int q, const uint4 c4, auto HEAD_, auto CAP_) __attribute__((always_inline)) {
+        constexpr bool HEAD = decltype(HEAD_)::value;  // lanes left of column 1 hold the border
+        constexpr bool CAP = decltype(CAP_)::value;    // the phase holds cell (m, n)
+        int INZ[16], INF[16];
+        if (q <= Bin) {
+          if (s == 0) {
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj) {
+              const int col = cs + 16 * q + jj;
+              INZ[jj] = col < 0 ? MSA_NEG : (col == 0 ? 3 : 2 - h4);
+              INF[jj] = col < 0 ? MSA_NEG : (col == 0 ? 3 - h4 : 2 - 2 * h4);
+            }
+          } else {
+            const lds_int4* srz = reinterpret_cast<const lds_int4*>(L(lds + 16 * (q - q0)));
+            const lds_int4* srf = reinterpret_cast<const lds_int4*>(L(lds + 256 + 16 * (q - q0)));
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const fl_v4i vz = srz[u], vf = srf[u];
+              INZ[4 * u] = vz.x; INZ[4 * u + 1] = vz.y; INZ[4 * u + 2] = vz.z; INZ[4 * u + 3] = vz.w;
+              INF[4 * u] = vf.x; INF[4 * u + 1] = vf.y; INF[4 * u + 2] = vf.z; INF[4 * u + 3] = vf.w;
+            }
+          }
+        } else {
+#pragma unroll
+          for (int jj = 0; jj < 16; ++jj) INZ[jj] = INF[jj] = MSA_NEG;
+        }
+        const unsigned cw[4] = {c4.x, c4.y, c4.z, c4.w};
+        unsigned dw[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const unsigned s4 = __builtin_amdgcn_perm(phi, plo, cw[u]);
+          unsigned word = 0;
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) {
+            const int kx = 4 * u + kk;
+            const int sc = ((int)(s4 << (24 - 8 * kk))) >> 24;
+            const int uH = dpp_shr1(INZ[kx], Hs);
+            const int uD = dpp_shr1(INF[kx], Ds);
+            const int t1 = (int)((unsigned)U | 3u) + sc;
+            const int t2 = (int)(((unsigned)Rs & ~3u) | 2u);
+            const int t3 = (int)(((unsigned)uD & ~3u) | 1u);
+            const unsigned dir = ((unsigned)U & 3u) | (((unsigned)Rs & 3u) << 2) | (((unsigned)uD & 3u) << 4);
+            word |= dir << (8 * kk);
+            const int t1h = t1 - h4;
+            int hh = imax3(t1, t2, t3);
+            int rr = imax3(t1h, t2, t3 - h4);
+            int dd = imax3(t1h, t2 - h4, t3);
+            asm("" : "+v"(hh));
+            if constexpr (HEAD) {
+              const bool before = 16 * q + kx < tmin;
+              hh = before ? 1 - h4 : hh;
+              rr = before ? 1 - 2 * h4 : rr;
+              dd = before ? 1 - h4 : dd;
+            }
+            if constexpr (CAP) {
+              if (16 * q + kx == tf) {
+                const int gmn = g * (m + n);  // unshift
+                msa_stripe_meta* md = a.meta + a.stripe0 + S - 1;
+                md->fin[0] = (t1 >> 2) - gmn;
+                md->fin[1] = (t2 >> 2) - gmn;
+                md->fin[2] = (t3 >> 2) - gmn;
+                md->has_fin = 1;
+              }
+            }
+            U = uH;
+            Hs = hh;
+            Rs = rr;
+            Ds = dd;
+          }
+          dw[u] = word;
+        }
+        __builtin_nontemporal_store(fl_v4u{dw[0], dw[1], dw[2], dw[3]}, dp + (size_t)q * 64);
+      };
+      using T_ = std::true_type;
+      using F_ = std::false_type;
+      for (int q = q0; q < q1; ++q) {
+        const uint4 c4 = cr0;
+        cr0 = cr1;
+        cr1 = cr2;
+        cr2 = cr3;
+        cr3 = ldc(q + 4);
+        const bool cap = __ballot(tf >= 16 * q && tf < 16 * q + 16) != 0ull;
+        if (cap) phase(q, c4, T_{}, T_{});
+        else if (q < 6) phase(q, c4, T_{}, F_{});
+        else phase(q, c4, F_{}, F_{});
+      }
+    }
+  }
+  if (lane == 0) a.blk[blk] = make_int4(0, 0, 0, 0);
 }
 
 // Pair result of a two-pass plan from the pass-2 block bests: every thread folds

@@ -783,6 +783,33 @@ def test_gotoh_device_walk(oracle, dev, LB, gh, st, en):
         assert min(tb["stop"]) == 0 and max(tb["stop"]) >= 0, tb["stop"]
 
 
+@pytest.mark.parametrize("gh", [(1, 2), (2, 1), (1, 0), (3, 5)])
+@pytest.mark.parametrize("m,n", [(1, 1), (1, 40), (5, 300), (64, 64), (65, 66), (129, 700), (1000, 1300), (2600, 900)])
+def test_gotoh_flow_dir_bytes(dev, LB, gh, m, n):
+    """The two-pass Gotoh flow kernel (single pair, start type -1, direction bytes: run_info mode 1) writes
+    the same tag byte as the one-pass stripe kernel (the same pair as a one-pair batch) at every cell, and
+    the same final-cell tables (score, find_alignment's end rule)."""
+    import torch
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+
+    g, h = gh
+    rng = np.random.default_rng(m * 3 + n + 17 * g + h)
+    A, B = _mutated(rng, m, n) if m > 100 else (rs(rng, m), rs(rng, n))
+    out = []
+    for single in (True, False):
+        pl = Plan(LB.REF_GOTOH, LB.CELLS_DIR, [m], [n], [0], [0], match=1, mismatch=0, gap_open=g + h,
+                  gap_extend=g, start_type=-1, single=single)
+        D = torch.empty(pl.cells_elems, dtype=torch.uint8, device=dev)
+        pl.run(_dev(A, dev), _dev(B, dev), D)
+        r = pl.results()[0]
+        out.append((pl.deskew_dir(D.cpu().numpy(), 0, pl.stripe_meta()), r["score"], tuple(r["fin"]),
+                    pl.run_info()["mode"]))
+    (d1, s1, f1, mode1), (d0, s0, f0, _) = out
+    assert mode1 == "flow"
+    assert (s1, f1) == (s0, f0)
+    assert np.array_equal(d1[1:, 1:] & 63, d0[1:, 1:] & 63)
+
+
 def test_gotoh_walk_rejects_wrong_plans(dev, LB):
     """msa_plan_traceback_gotoh needs a REF_GOTOH DIR plan and a valid end type; msa_plan_traceback needs an
     SW-affine DIR plan created with track_end (its walk starts at the fill's end cell)."""
