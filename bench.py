@@ -109,6 +109,20 @@ def cpu_baseline(wl: str, A: bytes, B: bytes, cores: int):
                 points=pts)
 
 
+def load_wave_time(wl: str):
+    """Where the DP kernel's waves spend their time (parked on s_waitcnt / barriers, issue-stalled,
+    issuing VALU / LDS / SALU; fractions of SQ_WAVE_CYCLES) from the newest committed PMC profile of
+    the workload (scripts/pmc_summary.py), or None."""
+    for p in sorted((REPO / "profiles").glob("*_pmc.json"), reverse=True):
+        try:
+            d = json.loads(p.read_text())
+        except Exception:
+            continue
+        if d.get("workload") == wl and d.get("wave_time"):
+            return dict(d["wave_time"], source=p.name)
+    return None
+
+
 def load_traffic(wl: str):
     """Per-launch HBM bytes of the DP kernel from the newest committed PMC profile
     (profiles/<round>_<wl>_pmc.json, scripts/pmc_summary.py: 2 x FETCH_SIZE + WRITE_SIZE per the
@@ -360,6 +374,7 @@ def main():
                         traffic=load_traffic(wl),
                         note=f"algorithmic ops = {OPS_PER_CELL[wl]:.0f} int32 ops/cell (SURVEY §8(d)) x cells / "
                              f"DP-kernel mean time {kern_ms:.4f} ms; peak = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz")
+        roof["pmc_wave_time"] = load_wave_time(wl)
         cpu = None
         if not args.no_cpu_baseline:
             try:

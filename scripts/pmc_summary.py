@@ -43,6 +43,18 @@ if "FETCH_SIZE" in pl or "WRITE_SIZE" in pl:
     fetch = 2.0 * pl.get("FETCH_SIZE", 0.0) * 1024.0
     write = pl.get("WRITE_SIZE", 0.0) * 1024.0
     out["hbm_bytes_per_launch"] = {"fetch_corrected": fetch, "write": write, "total": fetch + write}
+# where the DP kernel's waves spend their time (SQ counters summed over waves; WAIT_ANY +
+# WAIT_INST_ANY + ACTIVE_INST_ANY ~= WAVE_CYCLES, MI355X_MICROARCH.md "rocprofv3 PMC slots"):
+# parked on s_waitcnt / s_barrier, stalled at issue, issuing VALU, issuing LDS
+wc = pl.get("SQ_WAVE_CYCLES", 0.0)
+if wc > 0:
+    out["wave_time"] = {
+        "parked_waitcnt_or_barrier": round(pl.get("SQ_WAIT_ANY", 0.0) / wc, 4),
+        "issue_stall": round(pl.get("SQ_WAIT_INST_ANY", 0.0) / wc, 4),
+        "valu_active": round(pl.get("SQ_ACTIVE_INST_VALU", 0.0) / wc, 4),
+        "lds_active": round(pl.get("SQ_ACTIVE_INST_LDS", 0.0) / wc, 4),
+        "salu_active": round(pl.get("SQ_ACTIVE_INST_SCA", 0.0) / wc, 4),
+    }
 stats = src / "trace" / "run_kernel_stats.csv"
 if stats.exists():
     shutil.copy(stats, dst / f"{rnd}_{wl}_kernel_stats.csv")

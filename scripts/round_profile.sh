@@ -3,7 +3,7 @@
 # GPU parity tests, one bench line per workload, then rocprofv3 kernel stats + PMC
 # passes (scripts/prof.sh) for each workload; everything lands under gpurun_out/.
 set -o pipefail
-RND=${1:-r02}; WLS=${2:-"c2 c3 c4 c5"}
+RND=${1:-r03}; WLS=${2:-"c2 c3 c4 c5 ref"}
 mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/pytest_gpu.log; exit 1; }
 tail -2 gpurun_out/pytest_gpu.log
