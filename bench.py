@@ -390,7 +390,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if wl == "c4" else "weak",  # c4: a fixed 1024-pair batch split over ranks
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic i.i.d. ACGT" if syn else "gene_sequences_test (reference's bundled FASTA)",
