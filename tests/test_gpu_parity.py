@@ -810,6 +810,41 @@ def test_gotoh_flow_dir_bytes(dev, LB, gh, m, n):
     assert np.array_equal(d1[1:, 1:] & 63, d0[1:, 1:] & 63)
 
 
+@pytest.mark.parametrize("gap", [("B", 300), ("A", 300), ("B", 700), ("A", 70), ("both", 260)])
+def test_walks_across_long_gaps(oracle, dev, LB, gap):
+    """Long gaps move the walk out of its stripe group on the left (horizontal gap: an on-demand group of
+    the same stripe) or into a stripe far from the predicted column (vertical gap: mispredicted prefetches):
+    the reference Gotoh walk (flow kernel fill) and the SW-affine walk still equal the oracle."""
+    import torch
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+
+    side, L = gap
+    rng = np.random.default_rng(L + len(side))
+    X, Y, Z = rs(rng, 1500), rs(rng, 1200), rs(rng, L)
+    # (m <= n throughout: a Plan is not swapped the way Subproblem's constructor swaps; an extra tail on B
+    # keeps the vertical-gap case m <= n)
+    A, B = (X + Y, X + Z + Y) if side == "B" else \
+        ((X + Z + Y, X + Y + rs(rng, L + 50)) if side == "A" else (X + Z + Y, X + Y + Z))
+    m, n = len(A), len(B)
+    pl = Plan(LB.REF_GOTOH, LB.CELLS_DIR, [m], [n], [0], [0], match=1, mismatch=0, gap_open=3, gap_extend=1,
+              start_type=-1)
+    D = torch.empty(pl.cells_elems, dtype=torch.uint8, device=dev)
+    pl.run(_dev(A, dev), _dev(B, dev), D)
+    assert pl.run_info()["mode"] == "flow"
+    tb = pl.traceback_gotoh(D, end_type=-1)
+    o = oracle.subproblem_align(A, B, -1, -1, 1.0, 2.0)
+    want = "".join("MDI"[t - 1] for (_, _, t) in reversed(o["nodes"]))
+    assert tb["ops"].decode() == want
+    pl2 = Plan(LB.SW_AFFINE, LB.CELLS_DIR, [m], [n], [0], [0], match=2, mismatch=-1, gap_open=3, gap_extend=1,
+               track_end=True)
+    D2 = torch.empty(pl2.cells_elems, dtype=torch.uint8, device=dev)
+    pl2.run(_dev(A, dev), _dev(B, dev), D2)
+    tb2 = pl2.traceback(D2)
+    o2 = oracle.sw(A, B, 2, -1, 3, 1, want_tb=True)
+    assert (pl2.results()[0]["score"], tuple(tb2["beg"]), tb2["cigar"]) == (o2["score"], tuple(o2["beg"]),
+                                                                           o2["cigar"])
+
+
 def test_gotoh_walk_rejects_wrong_plans(dev, LB):
     """msa_plan_traceback_gotoh needs a REF_GOTOH DIR plan and a valid end type; msa_plan_traceback needs an
     SW-affine DIR plan created with track_end (its walk starts at the fill's end cell)."""
