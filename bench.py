@@ -275,6 +275,7 @@ def main():
 
     checks = {}
     dp_launch = None
+    gather_ms = None
     if wl == "c2":
         o = O.sw(A, B, 1, 0, 1, 1, want_h=(rank == 0))
         checks["score_matches_cpu"] = bool(o["score"] == res[0]["score"])
@@ -304,7 +305,9 @@ def main():
         inf = tb_info.cpu().tolist()
         fx = [c for c in json.loads((REPO / "tests" / "golden" / "at_size.json").read_text())
               if (c["a"], c["b"], c["L"], c["g"], c["h"]) == (0, 1, m, 1.0, 2.0)]
-        # the boundary call itself (host buffers in, text out), timed outside the device-resident steps
+        # the boundary call itself (host buffers in, text out), timed outside the device-resident steps,
+        # after one untimed call (its first call in this process fills the device-block pool)
+        api.main_alignment_text(b"\0" + A, b"\0" + B, m, n, 32, 1.0, 2.0)
         tb0 = time.perf_counter()
         for _ in range(3):
             text, sc = api.main_alignment_text(b"\0" + A, b"\0" + B, m, n, 32, 1.0, 2.0)
@@ -320,6 +323,18 @@ def main():
             o = O.main_alignment_text(A, B, 1.0, 2.0)
             checks["text_matches_cpu"] = bool(text == o[0])
     else:
+        # the score all-gather's share of a step (outside the timed region): the collective alone, on
+        # this rank's last scores
+        from cse305_parallel_sequence_alignment_amd.shard import gather_scores
+
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        g0 = time.perf_counter()
+        for _ in range(20):
+            gather_scores(local_scores, total, rank, world)
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - g0) / 20 * 1e3
         got = [int(x) for x in gathered.cpu().tolist()]
         fx = REPO / "tests" / "golden" / "c4_scores.json"
         if not syn and fx.exists():
@@ -404,6 +419,9 @@ def main():
                            **({"traceback_ms": round(tb_ms, 4), "traceback_walk": tb_walk} if tb_ms is not None
                               else {}),
                            **({"dp_launch": dp_launch} if dp_launch is not None else {}),
+                           **({"score_allgather_ms": round(gather_ms, 4),
+                               "score_allgather_share": round(gather_ms / (elapsed / args.steps * 1e3), 4)}
+                              if gather_ms is not None else {}),
                            **({"boundary_call_ms": round(boundary_ms, 3),
                                "boundary_note": "msa_main_alignment with host buffers (plan set-up, H2D codes, fill, "
                                                 "device walk, D2H ops, node list, print_seq text): PCIe-inclusive, "

@@ -5,7 +5,10 @@ The hot path has no cross-pair dependency: a batch of pairs (C4: 1024 pairs of
 fills its block with its own kernel launch.  The only collectives are the
 broadcast of the shared reference sequence (once) and the score all-gather at
 the end of every step (RCCL over xGMI on MI355X, gloo in the CPU tests) --
-there is no data-path exchange, so scaling is weak.
+there is no data-path exchange.  The batch is fixed and split over the ranks,
+so adding ranks shrinks each rank's share (strong scaling of the batch); below
+two workgroups' worth of pairs per CU a rank's plan splits every pair over
+several CUs (split mode).
 
 This mirrors how the reference parallelises *across* pairs
 (testing.cpp:112-158: one std::thread per pair, each calling
