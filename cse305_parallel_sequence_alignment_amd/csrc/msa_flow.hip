@@ -538,8 +538,10 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         }
       }
     } else if (k0 + w < S) {
+     // (two-value kinds: affine SW and Gotoh share this wave's protocol; the one-value SW-linear
+     // wave follows in the else branch)
      if constexpr (AFF) {
-      // =================== compute wave (affine): stripe k ===================
+      // =================== compute wave (affine / Gotoh): stripe k ===================
       const int k = k0 + w;
       const int cs = fl_cs(k);
       const int P = fl_P(k, m, n, 1);
@@ -701,19 +703,19 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
               xz[kx] = h;
               xf[kx] = dd;
             } else {
-            const int upZ = dpp_shr1(Z[kx >> 2][kx & 3], Zl);
-            const int upF = dpp_shr1(F[kx >> 2][kx & 3], Fo);
-            const int e = imax(E, Zl);
-            const int f = imax(upF, upZ);
-            const int d = imax(U + sc, flq + g * kx);
-            int h = imax3(d, e, f);
-            asm("" : "+v"(h));
-            U = upZ;
-            E = e;
-            Fo = f;
-            Zl = h - oe;
-            xz[kx] = Zl;
-            xf[kx] = f;
+              const int upZ = dpp_shr1(Z[kx >> 2][kx & 3], Zl);
+              const int upF = dpp_shr1(F[kx >> 2][kx & 3], Fo);
+              const int e = imax(E, Zl);
+              const int f = imax(upF, upZ);
+              const int d = imax(U + sc, flq + g * kx);
+              int h = imax3(d, e, f);
+              asm("" : "+v"(h));
+              U = upZ;
+              E = e;
+              Fo = f;
+              Zl = h - oe;
+              xz[kx] = Zl;
+              xf[kx] = f;
             }
           }
         }
@@ -755,7 +757,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
           done = true;
         }
       }
-      if (!done) {
+      if (!done) {  // (the SW-linear wave's loop shape below)
       for (; q + 1 < qa; q += 2) {
         run_phase(q, ZA, FA, CAl, CAh, ZB, FB, CBl, CBh, F_{}, F_{});
         run_phase(q + 1, ZB, FB, CBl, CBh, ZA, FA, CAl, CAh, F_{}, F_{});
