@@ -55,8 +55,20 @@ namespace msa {
 #ifndef FL_FSLEEP
 #define FL_FSLEEP 32    // s_sleep between a pass-2 wave's polls of its block's last granule
 #endif
+#ifndef FL_PUBLATE
+#define FL_PUBLATE 0    // 1: the producer-counter read is awaited after the hand-off, with the data
+#endif
+#ifndef FL_HO
+#define FL_HO 0         // SW-linear hand-off: 0 = 16 ds_write_addtid_b32, 1 = 8 ds_write_b64
+#endif
 #ifndef FL_IOSLEEP
 #define FL_IOSLEEP 1    // s_sleep of an idle io wave
+#endif
+// Diagnostic builds only (-DMSA_ABL=mask; results are wrong): 1 no pass-2 work, 2 no SNAP
+// stores, 4 io-out stores no bottom rows (granules still), 16 SW-linear compute waves never wait on their producer
+// or consumers (each stripe runs at its own speed), 32 never on the producer, 64 never on consumers
+#ifndef MSA_ABL
+#define MSA_ABL 0
 #endif
 
 __host__ __device__ __forceinline__ int fl_cs(int k) { return -((16 - (k & 15)) & 15); }  // -((-k) mod 16)
@@ -159,6 +171,28 @@ __device__ __forceinline__ void ds_handoff_tid(unsigned long long m63, unsigned 
         [x5] "v"(x[5]), [x6] "v"(x[6]), [x7] "v"(x[7]), [x8] "v"(x[8]), [x9] "v"(x[9]), [x10] "v"(x[10]),
         [x11] "v"(x[11]), [x12] "v"(x[12]), [x13] "v"(x[13]), [x14] "v"(x[14]), [x15] "v"(x[15]), [pa] "v"(pa),
         [pv] "v"(pv)
+      : "memory");
+}
+
+// The same hand-off as 8 single-lane ds_write_b64 + the counter (9 DS ops instead of 17: with
+// the phase's 6 prefetch reads in flight, 23 outstanding DS ops exceed the 15 lgkmcnt tracks)
+typedef int fl_v2i __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void ds_handoff_b64(unsigned long long m63, unsigned addr, const int (&x)[16], unsigned pa,
+                                               int pv) {
+  unsigned long long sv;
+  const fl_v2i x0{x[0], x[1]}, x1{x[2], x[3]}, x2{x[4], x[5]}, x3{x[6], x[7]};
+  const fl_v2i x4{x[8], x[9]}, x5{x[10], x[11]}, x6{x[12], x[13]}, x7{x[14], x[15]};
+  asm volatile(
+      "s_mov_b64 %[sv], exec\n\ts_mov_b64 exec, %[m]\n\t"
+      "ds_write_b64 %[a], %[x0] offset:0\n\tds_write_b64 %[a], %[x1] offset:8\n\t"
+      "ds_write_b64 %[a], %[x2] offset:16\n\tds_write_b64 %[a], %[x3] offset:24\n\t"
+      "ds_write_b64 %[a], %[x4] offset:32\n\tds_write_b64 %[a], %[x5] offset:40\n\t"
+      "ds_write_b64 %[a], %[x6] offset:48\n\tds_write_b64 %[a], %[x7] offset:56\n\t"
+      "ds_write_b32 %[pa], %[pv]\n\t"
+      "s_mov_b64 exec, %[sv]\n\ts_nop 4"
+      : [sv] "=&s"(sv)
+      : [m] "s"(m63), [a] "v"(addr), [x0] "v"(x0), [x1] "v"(x1), [x2] "v"(x2), [x3] "v"(x3), [x4] "v"(x4),
+        [x5] "v"(x5), [x6] "v"(x6), [x7] "v"(x7), [pa] "v"(pa), [pv] "v"(pv)
       : "memory");
 }
 
@@ -340,6 +374,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
     if (threadIdx.x == 0) smem[1] = atomicAdd(a.ticket + 13, 1);
     __syncthreads();
     if (uni(smem[1]) >= a.nflow) {
+      if constexpr ((MSA_ABL & 1) != 0) return;
       // pass-2 workgroup: every wave takes blocks on its own, in expected readiness order
       for (;;) {
         // (a separate, non-inlined block function keeps this loop's control flow
@@ -512,7 +547,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
             const int blk = bl[l] + j;
             const int v = *(const lds_int*)(rings + l * 256 * NV + (blk & (FL_RINGB - 1)) * 16 + c);
             const int vf = AFF ? *(const lds_int*)(rings + l * 256 * NV + 256 + (blk & (FL_RINGB - 1)) * 16 + c) : 0;
-            if (SAVE) {
+            if (SAVE && (MSA_ABL & 4) == 0) {
               gstore(a.br + (size_t)(kc - 1) * a.brw + 16 * blk + c, ((unsigned long long)ep << 32) | (unsigned)v);
               if constexpr (AFF)
                 gstore(a.br + (size_t)(S_br + kc - 1) * a.brw + 16 * blk + c,
@@ -606,9 +641,12 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
           val = uni(v);
           if (val < need) {
             __builtin_amdgcn_s_sleep(0);
-            if (++spins > FL_SPIN_MAX) { if (lane == 0) atomicExch(a.err, 12); break; }
+            if (++spins > FL_SPIN_MAX) break;
           }
         }
+        // (reported after the loop: a divergent store inside it would make the loop's
+        // values divergent, i.e. VGPRs and exec-mask branches on the hot path)
+        if (val < need && lane == 0) atomicExch(a.err, 12);
       };
       auto refresh_cons = [&](int need) __attribute__((always_inline)) {
         while (consv < need) {
@@ -619,9 +657,10 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
           consv = uni(min(c1, c2));
           if (consv < need) {
             __builtin_amdgcn_s_sleep(0);
-            if (++spins > FL_SPIN_MAX) { if (lane == 0) atomicExch(a.err, 13); break; }
+            if (++spins > FL_SPIN_MAX) break;
           }
         }
+        if (consv < need && lane == 0) atomicExch(a.err, 13);
       };
       auto mask_in = [&](int q, fl_v4i (&Z)[4], fl_v4i (&F)[4]) __attribute__((always_inline)) {
         if (q > Bin) {  // past the producer's last column (all > n)
@@ -854,18 +893,35 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
       auto reread_in = [&](int q, fl_v4i (&IN)[4]) __attribute__((always_inline)) {
         ds_reread_b128x4(a_ring_in + (unsigned)((q & (FL_RINGB - 1)) * 64), IN);
       };
+#ifdef MSA_STAMPS
+      unsigned long long tw_in = 0, tw_cons = 0;  // s_memtime ticks in the two wait loops
+      int ncons = 0;
+#endif
       auto wait_flag = [&](unsigned addr, int& val, int need) __attribute__((always_inline)) {
+#ifdef MSA_STAMPS
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
         while (val < need) {
           int v = ds_read_b32(addr);
           lgkm_wait<0>(v);
           val = uni(v);
           if (val < need) {
             __builtin_amdgcn_s_sleep(0);
-            if (++spins > FL_SPIN_MAX) { if (lane == 0) atomicExch(a.err, 12); break; }
+            if (++spins > FL_SPIN_MAX) break;
           }
         }
+        // (reported after the loop: a divergent store inside it would make the loop's
+        // values divergent, i.e. VGPRs and exec-mask branches on the hot path)
+        if (val < need && lane == 0) atomicExch(a.err, 12);
+#ifdef MSA_STAMPS
+        tw_in += __builtin_amdgcn_s_memtime() - t0;
+#endif
       };
       auto refresh_cons = [&](int need) __attribute__((always_inline)) {
+#ifdef MSA_STAMPS
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+        ++ncons;
+#endif
         while (consv < need) {
           int c1 = ds_read_b32(a_cons1);
           int c2 = ds_read_b32(a_cons2);
@@ -874,9 +930,13 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
           consv = uni(two_cons ? min(c1, c2) : c1);
           if (consv < need) {
             __builtin_amdgcn_s_sleep(0);
-            if (++spins > FL_SPIN_MAX) { if (lane == 0) atomicExch(a.err, 13); break; }
+            if (++spins > FL_SPIN_MAX) break;
           }
         }
+        if (consv < need && lane == 0) atomicExch(a.err, 13);
+#ifdef MSA_STAMPS
+        tw_cons += __builtin_amdgcn_s_memtime() - t0;
+#endif
       };
       auto mask_in = [&](int q, fl_v4i (&IN)[4]) __attribute__((always_inline)) {
         if (q > Bin) {  // past the producer's last column (all > n)
@@ -902,7 +962,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
           __attribute__((always_inline)) {
         constexpr bool MASK = decltype(MASK_)::value;  // phase q+1 may lie past the producer's last block
         const int need = MASK ? min(q + 1, Bin + 1) : q + 1;
-        if (pubv - dq_in < need) {
+        if (__builtin_expect((MSA_ABL & 48) == 0 && pubv - dq_in < need, 0)) {
 #ifdef MSA_STAMPS
           ++nslow;
 #endif
@@ -910,7 +970,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
           reread_in(q, IN);
           if constexpr (MASK) mask_in(q, IN);
         }
-        if constexpr (SAVE) {
+        if constexpr (SAVE && (MSA_ABL & 2) == 0) {
           if (q % FL_PS == 0) {  // pass 2 restarts here: each lane's left and diagonal values
             unsigned long long* sp = a.snap + ((size_t)k * a.nseg + q / FL_PS) * (128 * R) + lane;
             gstore(sp, ((unsigned long long)ep << 32) | (unsigned)X);
@@ -957,18 +1017,29 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
 #pragma unroll
           for (int kx = 0; kx < 16; kx += 2) best = imax3(best, hv[kx], hv[kx + 1]);
         }
+#if !FL_PUBLATE
         lgkm_wait<5>(pubn);  // the counter read (oldest of the six) has landed
         pubv = uni(pubn);
+#endif
         // hand-off: lane 63's 16 values of this phase = block q - dq of the out ring
         const int bq = q - dq;
         const bool wr = has_out && bq >= 0;
-        if (wr && consv < bq - (FL_RINGB - 1)) refresh_cons(bq - (FL_RINGB - 1));
+        if (__builtin_expect((MSA_ABL & 80) == 0 && wr && consv < bq - (FL_RINGB - 1), 0))
+          refresh_cons(bq - (FL_RINGB - 1));
         const unsigned wa = wr ? a_ring_out + (unsigned)((bq & (FL_RINGB - 1)) * 64) : a_dummy;
+#if FL_HO == 1
+        ds_handoff_b64(m63, wa, xo, a_prog_me, q + 1);
+#else
         ds_handoff_tid(m63, wa - 252u, xo, a_prog_me, q + 1);  // (-6.5% on C2 vs four single-lane b128 writes)
+#endif
 #ifdef MSA_STAMPS
         if (q == dq) FL_STAMP(0, 3, __builtin_amdgcn_s_memrealtime());
 #endif
         lgkm_wait_v<5>(INn, CWn);  // phase q+1's prefetched inputs have landed (the writes may fly)
+#if FL_PUBLATE
+        lgkm_wait<5>(pubn);  // (landed with them: it was read first)
+        pubv = uni(pubn);
+#endif
         if constexpr (MASK) mask_in(q + 1, INn);
       };
       using T_ = std::true_type;
@@ -999,6 +1070,9 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
       lgkm_wait_v<0>(INb, CWb);
       FL_STAMP(0, 1, __builtin_amdgcn_s_memrealtime());
       FL_STAMP(0, 2, (unsigned long long)nslow);
+      FL_STAMP(1, 0, tw_in);
+      FL_STAMP(1, 1, tw_cons);
+      FL_STAMP(1, 2, (unsigned long long)ncons);
       // ---- stripe finalize ----
       msa_stripe_meta* md = a.meta + pd.stripe0 + k;
       if constexpr (BEST) {

@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Diagnostic (needs a -DMSA_STAMPS build of libmsa.so, optionally with -DMSA_ABL ablations):
+per-stripe start / end times and slow-path phase counts of a flow kernel's pass 1 (items < 64),
+for the C2 (SW linear, H, two rows per lane), C5 (SW affine, direction bytes) or ref
+(Gotoh, tag bytes) single pair.  Prints one JSON summary line.
+
+    python3 scripts/stamps_flow.py --workload c2 [--tag name]
+"""
+import argparse
+import ctypes as C
+import json
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import numpy as np
+import torch
+
+from cse305_parallel_sequence_alignment_amd import _lib as LB, data
+from cse305_parallel_sequence_alignment_amd.plan import Plan
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--workload", default="c2", choices=["c2", "c5", "ref"])
+ap.add_argument("--tag", default="")
+args = ap.parse_args()
+wl = args.workload
+if wl == "c2":
+    A, B = data.c2_pair(0)
+    pl = Plan(LB.SW_LINEAR, LB.CELLS_H, [len(A)], [len(B)], [0], [0], match=1, mismatch=0, gap_open=1, gap_extend=1)
+    out = torch.empty(pl.cells_elems, dtype=torch.int32, device="cuda")
+    rows = 128
+elif wl == "c5":
+    A, B = data.c5_pair(0)
+    pl = Plan(LB.SW_AFFINE, LB.CELLS_DIR, [len(A)], [len(B)], [0], [0], match=1, mismatch=0, gap_open=3,
+              gap_extend=1, track_end=True)
+    out = torch.empty(pl.cells_elems, dtype=torch.uint8, device="cuda")
+    rows = 64
+else:
+    A, B = data.bundled()[0][:10000], data.bundled()[1][:10000]
+    pl = Plan(LB.REF_GOTOH, LB.CELLS_DIR, [len(A)], [len(B)], [0], [0], match=1, mismatch=0, gap_open=3,
+              gap_extend=1, start_type=-1)
+    out = torch.empty(pl.cells_elems, dtype=torch.uint8, device="cuda")
+    rows = 64
+dA = torch.from_numpy(data.encode(A)).cuda()
+dB = torch.from_numpy(data.encode(B)).cuda()
+st = torch.zeros(64 * 16 * 4096 * 4, dtype=torch.int64, device="cuda")
+lib = LB.lib()
+lib.msa_debug_stamps.argtypes = [C.c_void_p, C.c_void_p]
+kms = []
+for rep in range(4):
+    st.zero_()
+    lib.msa_debug_stamps(pl._h, C.c_void_p(st.data_ptr()))
+    pl.run(dA, dB, out)
+    torch.cuda.synchronize()
+    kms.append(pl.kernel_ms())
+full = st.cpu().numpy().reshape(64, 16, 4096, 4)
+s = full[:, :4, 0, :]  # item, wave, slot
+wq = full[:, :4, 1, :]  # SW-linear waves: ticks waiting on the producer, on consumers, consumer waits
+t0 = s[0, 0, 0]
+recs = []
+for it in range(64):
+    for w in range(4):
+        a, b, ns = s[it, w, 0], s[it, w, 1], s[it, w, 2]
+        if a == 0:
+            continue
+        recs.append((4 * it + w, (a - t0) / 100.0, (b - t0) / 100.0, (b - a) / 100.0, int(ns)))
+ks = np.array([r[0] for r in recs])
+starts = np.array([r[1] for r in recs])
+durs = np.array([r[3] for r in recs])
+lag = np.diff(starts)
+P0 = (len(B) + 63) // 16 + 1
+out = dict(tag=args.tag, workload=wl, kernel_ms=[round(x, 4) for x in kms], stripes=len(recs),
+           dur0_us=round(float(durs[0]), 2), phase0_us=round(float(durs[0]) / P0, 4),
+           cycles_per_step0=round(float(durs[0]) / P0 / 16 * 2400, 1),
+           dur_by_wave_us=[round(float(durs[ks % 4 == w].mean()), 2) for w in range(4)],
+           dur_mean_us=round(float(durs.mean()), 2), dur_max_us=round(float(durs.max()), 2),
+           lag_intra_us=round(float(lag[(ks[1:] % 4) != 0].mean()), 3) if len(lag) else None,
+           lag_inter_us=round(float(lag[(ks[1:] % 4) == 0].mean()), 3) if len(lag) else None,
+           last_end_us=round(float(max(r[2] for r in recs)), 2),
+           slow_by_wave=[round(float(np.mean([r[4] for r in recs if r[0] % 4 == w])), 1) for w in range(4)],
+           rows_per_stripe=rows,
+           wait_in_ticks_s0=int(wq[0, 0, 0]), wait_cons_ticks_s0=int(wq[0, 0, 1]), ncons_s0=int(wq[0, 0, 2]),
+           wait_in_ticks_mean=float(np.mean([wq[r[0] // 4, r[0] % 4, 0] for r in recs])),
+           wait_cons_ticks_mean=float(np.mean([wq[r[0] // 4, r[0] % 4, 1] for r in recs])),
+           ncons_mean=float(np.mean([wq[r[0] // 4, r[0] % 4, 2] for r in recs])))
+print(json.dumps(out), flush=True)
