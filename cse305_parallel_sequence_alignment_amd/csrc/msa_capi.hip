@@ -1028,7 +1028,8 @@ int msa_plan_traceback(msa_plan* P, int64_t pair, const uint8_t* dDir, uint8_t* 
   hipStream_t st = (hipStream_t)stream;
   P->note_stream(st);
   hipLaunchKernelGGL(traceback_kernel<TB_SW>, dim3(1), dim3(64), 0, st, dDir, P->d_pairs, P->d_meta,
-                     (const PairResult*)P->d_res, (int)pair, 0, 0, d_ops, (long long)ops_cap, (long long*)d_info);
+                     (const PairResult*)P->d_res, (int)pair, 0, 0, d_ops, (long long)ops_cap, (long long*)d_info,
+                     P->flow ? 1 : 0);
   HIPCHK(hipGetLastError());
   return MSA_OK;
 }
@@ -1044,7 +1045,7 @@ int msa_plan_traceback_gotoh(msa_plan* P, int64_t pair, int end_type, const uint
   // REF1 bytes hold tags (3 / 2 / 1 = T1 / T2 / T3), REF bytes the table numbers
   hipLaunchKernelGGL(P->kp.alg == MSA_ALG_REF1 ? traceback_kernel<TB_REF_TAG> : traceback_kernel<TB_REF>, dim3(1),
                      dim3(64), 0, st, dDir, P->d_pairs, P->d_meta, (const PairResult*)P->d_res, (int)pair, end_type,
-                     (int)P->kp.h, d_ops, (long long)ops_cap, (long long*)d_info);
+                     (int)P->kp.h, d_ops, (long long)ops_cap, (long long*)d_info, P->flow ? 1 : 0);
   HIPCHK(hipGetLastError());
   return MSA_OK;
 }

@@ -170,7 +170,7 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
                                                        const msa_stripe_meta* __restrict__ meta,
                                                        const PairResult* __restrict__ res, int pair, int end_type,
                                                        int hpen, uint8_t* __restrict__ ops, long long cap,
-                                                       long long* __restrict__ info) {
+                                                       long long* __restrict__ info, int csflow) {
   constexpr bool REF = KIND != TB_SW;
   const int lane = threadIdx.x;
   const msa_pair_desc pd = pairs[pair];
@@ -196,8 +196,11 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
   constexpr int TB_CSL = 8192;
   __shared__ int csl[TB_CSL];
   const int S = (pd.m + 63) / 64;
-  for (int k = lane; k < S && k < TB_CSL; k += 64) csl[k] = meta[pd.stripe0 + k].cs;
+  if (!csflow)
+    for (int k = lane; k < S && k < TB_CSL; k += 64) csl[k] = meta[pd.stripe0 + k].cs;
   auto cs_of = [&](int k) {  // wave-uniform (readfirstlane: an LDS value is otherwise "divergent")
+    // the flow kernels' stripes start at fl_cs(k) = -((-k) mod 16): no LDS round trip
+    if (csflow) return -((16 - (k & 15)) & 15);
     return k < TB_CSL ? __builtin_amdgcn_readfirstlane(csl[k]) : meta[pd.stripe0 + k].cs;
   };
   // The walk records one word per window -- nibble q (from the top) = the lane step of step q
@@ -252,7 +255,8 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
   int slot_e0 = 0, slot_e1 = 0, slot_e2 = 0, slot_e3 = 0;
   int issued = 0;
   auto sel4 = [](int k, int a, int b, int c, int d) __attribute__((always_inline)) {
-    return k == 0 ? a : (k == 1 ? b : (k == 2 ? c : d));
+    const int lo = (k & 1) ? b : a, hi = (k & 1) ? d : c;  // (three selects, no branches)
+    return (k & 2) ? hi : lo;
   };
   auto set4 = [](int k, int v, int& a, int& b, int& c, int& d) __attribute__((always_inline)) {
     a = k == 0 ? v : a;
@@ -285,7 +289,8 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
   };
   int n_switch = 0, n_sync = 0;  // groups staged for the walk, of them on demand
 #ifdef MSA_TB_STATS
-  long long n_run = 0, n_win = 0, t_win = 0;  // diagnostic build: runs, windows, ticks inside groups
+  long long n_run = 0, n_win = 0, t_win = 0, t_pf = 0;  // diagnostic build: runs, windows, ticks inside
+                                                        // groups, ticks prefetching
 #endif
   long long t_wait = 0;  // diagnostic build: clock ticks spent waiting for group loads
   const long long t_begin = (long long)__builtin_amdgcn_s_memtime();
@@ -334,6 +339,9 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
         t_wait += (long long)__builtin_amdgcn_s_memtime() - a;
 #endif
       }
+#ifdef MSA_TB_STATS
+      const long long tp0 = (long long)__builtin_amdgcn_s_memtime();
+#endif
       if (entered) {
         // prefetch the next three stripes' groups (only s - 3 is new in steady state): a
         // diagonal path from (i, j) enters stripe s - d at column j - r - 64d + 63, step
@@ -349,6 +357,7 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
       int tg = t - 16 * b0;
 #ifdef MSA_TB_STATS
       const long long tw0 = (long long)__builtin_amdgcn_s_memtime();
+      t_pf += tw0 - tp0;
 #endif
       int sh = 10 * st;
       for (;;) {
@@ -439,7 +448,9 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
     info[4] = n_switch;
     info[5] = n_sync;
 #ifdef MSA_TB_STATS
+    info[2] = t_pf;
     info[3] = n_run;
+    info[4] = t_wait;
     info[5] = n_win;
     info[7] = t_win;
 #endif
