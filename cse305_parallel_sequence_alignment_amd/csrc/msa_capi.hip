@@ -304,9 +304,13 @@ kfn_t pick_kernel(int alg, int out, int tp, bool sgl) {
 }
 
 // single-pair SW linear (msa_flow.hip): pass 1 (chain), pass 2 (fill + H)
-kfn_t pick_flow(int alg, bool best, bool save, int tp, int R) {
-  // SW affine / the reference's Gotoh (direction bytes): pass 1 + in-launch pass 2, one row per lane
-  if (alg == MSA_ALG_SWA) return (save && R == 1) ? flow_kernel<true, false, true, true, 1, 1> : nullptr;
+kfn_t pick_flow(int alg, bool best, bool save, int tp, int R, bool nneg) {
+  // SW affine / the reference's Gotoh (direction bytes): pass 1 + in-launch pass 2, one row per lane;
+  // SW affine with scores >= 0: pass 1 applies the zero floor in its head phases only
+  if (alg == MSA_ALG_SWA) {
+    if (!save || R != 1) return nullptr;
+    return nneg ? flow_kernel<false, false, true, true, 1, 1> : flow_kernel<true, false, true, true, 1, 1>;
+  }
   if (alg == MSA_ALG_REF1) return (save && R == 1) ? flow_kernel<true, false, true, true, 1, 2> : nullptr;
   // score-only plans: pass 1 alone, one row per lane, best cell tracked in the chain;
   // H plans: pass 1 + in-launch pass 2, two rows per lane
@@ -537,7 +541,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   P->threads = (flow ? W + 2 : W + 1 + (single ? 1 : 0)) * 64;
   // rows per lane of the flow kernel (two-pass plans): 2 halves the inter-wave hand-offs per row
   P->R = (flow && out_mode == MSA_OUT_H) ? 2 : 1;
-  P->fn = flow ? pick_flow(kalg, out_mode == MSA_OUT_NONE, P->flow2, tp, P->R)
+  P->fn = flow ? pick_flow(kalg, out_mode == MSA_OUT_NONE, P->flow2, tp, P->R, desc->match >= 0 && desc->mismatch >= 0)
                : pick_kernel(kalg, out_mode, tp, single);
   if (!P->fn) { delete P; return MSA_ERR_UNSUPPORTED; }
   P->nc = nc_of(kalg);

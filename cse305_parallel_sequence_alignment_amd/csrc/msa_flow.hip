@@ -289,7 +289,8 @@ __device__ __forceinline__ int fl_step(int in, int s, int& X, int& U, int g) {
   return h;
 }
 
-// FLOOR: scores may be negative (zero floor, X-space); otherwise G-space.
+// FLOOR: scores may be negative (zero floor, X-space); otherwise G-space.  Affine SW: the
+// floor in every pass-1 step; otherwise (scores >= 0) only in the head phases.
 // BEST: track the best cell in pass 1 (score-only plans: no pass 2).
 // SAVE: write BR and SNAP for pass 2.
 // AFF: Smith-Waterman with affine gaps (config C5), pass 2 writing direction bytes.  Values
@@ -746,7 +747,10 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
               const int upF = dpp_shr1(F[kx >> 2][kx & 3], Fo);
               const int e = imax(E, Zl);
               const int f = imax(upF, upZ);
-              const int d = imax(U + sc, flq + g * kx);
+              // the floor e(i+j) (H = 0, a local start): with scores >= 0 (!FLOOR) the diagonal
+              // term of every real cell is already >= it (H~diag + s + 2e >= e(i+j)), so only the
+              // head phases, where lanes still hold virtual columns left of column 1, need it
+              const int d = (FLOOR || HEAD) ? imax(U + sc, flq + g * kx) : U + sc;
               int h = imax3(d, e, f);
               asm("" : "+v"(h));
               U = upZ;
@@ -780,8 +784,9 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
       const int qa = max(0, min(P, Bin));
       int q = 0;
       bool done = false;
-      if constexpr (GOT) {
+      if constexpr (GOT || (AFF && !FLOOR)) {
         // head: phases 0..5 (steps < 96 > every lane's tmin <= 79) hold the column-0 border
+        // (affine SW without the floor: the phases that still need it)
         if (qa >= 6) {
           for (; q < 6; q += 2) {
             run_phase(q, ZA, FA, CAl, CAh, ZB, FB, CBl, CBh, F_{}, T_{});

@@ -653,11 +653,12 @@ def test_c5_fill_and_device_traceback_20k(oracle, dev, LB, which):
 
 
 @pytest.mark.parametrize("m,n", [(1, 1), (64, 1), (1, 300), (65, 70), (300, 257), (1000, 1300), (2600, 900)])
-@pytest.mark.parametrize("scoring", [(1, 0, 3, 1), (2, -3, 5, 2), (1, -1, 1, 1), (3, -2, 0, 0)])
+@pytest.mark.parametrize("scoring", [(1, 0, 3, 1), (2, -3, 5, 2), (1, -1, 1, 1), (3, -2, 0, 0), (2, 0, 5, 2), (1, 1, 0, 0)])
 def test_sw_affine_flow_dir_bytes(dev, LB, m, n, scoring):
     """The two-pass affine flow kernel (single pair, direction bytes: run_info mode 1) writes the same
     direction byte as the one-pass stripe kernel (the same pair as a one-pair batch) at every cell of the
-    matrix, and the same score and first-maximum end cell."""
+    matrix, and the same score and first-maximum end cell.  Scores >= 0 run pass 1 with the zero floor in
+    its head phases only; negative mismatches with it in every step."""
     import torch
     from cse305_parallel_sequence_alignment_amd.plan import Plan
 
