@@ -353,7 +353,10 @@ struct msa_plan {
   // device
   msa_pair_desc* d_pairs = nullptr;
   msa_stripe_meta* d_meta = nullptr;
-  int* d_ticket = nullptr;  // [0] ticket, [4..11] per-XCD item chunks, [12] pass-2 blocks (reset every run)
+  // [0] ticket, [4..11] per-XCD item chunks; flow kernels: [32] arrival, [64] pass-2 blocks, each
+  // in a 128-byte line of its own (thousands of pass-2 waves claim blocks while pass-1 workgroups
+  // claim their items: on one line the item claims queued ~16 us behind them).  Reset every run.
+  int* d_ticket = nullptr;
   int* d_err = nullptr;     // sticky error word: set by a kernel wait that hit its spin limit; cleared
                             // only at plan creation and by msa_plan_clear_error
   unsigned long long* d_gbuf = nullptr;
@@ -764,7 +767,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     return fail();
   if (hipMemset(P->d_meta, 0, sizeof(msa_stripe_meta) * std::max<int64_t>(1, P->total_stripes)) != hipSuccess)
     return fail();
-  if (!P->alloc(&P->d_ticket, 64)) return fail();
+  if (!P->alloc(&P->d_ticket, 4 * MSA_NTICKET)) return fail();
   if (!P->alloc(&P->d_err, 64) || hipMemset(P->d_err, 0, 64) != hipSuccess) return fail();
   if (!P->alloc(&P->d_cod, (size_t)MSA_NCOPY * P->cod_copy + 64)) return fail();
   if (!P->alloc(&P->d_segs, sizeof(msa_pair_desc) * P->segs.size())) return fail();

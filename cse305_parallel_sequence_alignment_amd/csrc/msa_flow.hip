@@ -366,22 +366,37 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
   const unsigned ep = kp.epoch;
   const int grp = (int)(blockIdx.x & 7), chunk = kp.sched_cap;
 
+#ifdef MSA_STAMPS
+  // workgroup lifetimes: item 63 / wave 15's area, q = blockIdx.x: slot 0 start, 1 end, 2 role
+  auto wg_stamp = [&](int slot, unsigned long long v) {
+    if (a.stamps && threadIdx.x == 0 && blockIdx.x < 4096)
+      a.stamps[(((size_t)63 * 16 + 15) * 4096 + blockIdx.x) * 4 + slot] = v;
+  };
+  wg_stamp(0, __builtin_amdgcn_s_memrealtime());
+#endif
   if constexpr (SAVE) {
     // Role by arrival, not by blockIdx: the first nflow workgroups to START run pass 1,
     // the later ones pass-2 blocks.  A pass-2 block waits only on pass-1 outputs, and
     // every pass-1 role is held by a workgroup that is already running (and stays
     // resident until every item is claimed), so progress does not depend on the order
     // in which the hardware dispatches workgroups, or on CUs held by other kernels.
-    if (threadIdx.x == 0) smem[1] = atomicAdd(a.ticket + 13, 1);
+    if (threadIdx.x == 0) smem[1] = atomicAdd(a.ticket + MSA_TK_ARRIVE, 1);
     __syncthreads();
+#ifdef MSA_STAMPS
+    if (a.stamps && threadIdx.x == 0 && blockIdx.x < 2048)
+      a.stamps[(((size_t)63 * 16 + 15) * 4096 + 2048 + blockIdx.x) * 4 + 0] = __builtin_amdgcn_s_memrealtime();
+#endif
     if (uni(smem[1]) >= a.nflow) {
+#ifdef MSA_STAMPS
+      wg_stamp(2, 2);
+#endif
       if constexpr ((MSA_ABL & 1) != 0) return;
       // pass-2 workgroup: every wave takes blocks on its own, in expected readiness order
       for (;;) {
         // (a separate, non-inlined block function keeps this loop's control flow
         // uniform: inlined, the structurizer re-entered it without the ticket)
         int t = 0;
-        if (lane == 0) t = atomicAdd(a.ticket + 12, 1);
+        if (lane == 0) t = atomicAdd(a.ticket + MSA_TK_BLOCK, 1);
         t = __builtin_amdgcn_readlane(t, 0);
         if (t >= a.nblk) break;
         const FillArgs f{a.A, a.cod, a.br, a.snap, a.outH, a.blk, a.err, a.cod_copy, a.pairs[0].a_off,
@@ -392,6 +407,9 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         else if constexpr (AFF) fill_block_aff(f, a.border[t], lane, smem + w * 544);
         else fill_block<FLOOR, TRACKPOS, R>(f, a.border[t], lane, smem + w * 544);
       }
+#ifdef MSA_STAMPS
+      wg_stamp(1, __builtin_amdgcn_s_memrealtime());
+#endif
       return;
     }
   }
@@ -415,6 +433,12 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
     if (threadIdx.x >= 16 && threadIdx.x < 128) flags[threadIdx.x] = 0;
     __syncthreads();
     const int item = uni(flags[0]);
+#ifdef MSA_STAMPS
+    if (a.stamps && threadIdx.x == 0 && blockIdx.x < 2048 && item < kp.n_items) {
+      a.stamps[(((size_t)63 * 16 + 15) * 4096 + 2048 + blockIdx.x) * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+      a.stamps[(((size_t)63 * 16 + 15) * 4096 + 2048 + blockIdx.x) * 4 + 2] = item + 1;
+    }
+#endif
     if (item >= kp.n_items) break;
     const int k0 = item * W;
 
@@ -449,6 +473,10 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         Yr = max(Yr, Y1);
       };
       load_codes(1024);
+#ifdef MSA_STAMPS
+      __builtin_amdgcn_s_waitcnt(0);
+      FL_STAMP(0, 0, __builtin_amdgcn_s_memrealtime());
+#endif
       const unsigned long long* g_in = a.gbuf + (size_t)(item > 0 ? item - 1 : 0) * NV * a.gbuf_stride;
       int b = 0;
       int consv = 0;
@@ -1103,6 +1131,10 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
     }
     __syncthreads();
   }
+#ifdef MSA_STAMPS
+  wg_stamp(2, 1);
+  wg_stamp(1, __builtin_amdgcn_s_memrealtime());
+#endif
 }
 
 // Pass 2: block (stripe s, segment seg) of FL_PS phases, one wave.  Its inputs

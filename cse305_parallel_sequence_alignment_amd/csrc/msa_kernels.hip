@@ -67,6 +67,9 @@
 #define MSA_GOFF 128
 #define MSA_NEG (-(1 << 30))
 #define MSA_VIRT_CODE 7u     // SW: column code outside [1, n] (real symbols use codes 0..6)
+#define MSA_NTICKET 128      // run tickets (ints): [0] stripe_kernel, [4..11] flow item chunks,
+#define MSA_TK_ARRIVE 32     // flow kernel: arrival order (pass-1 / pass-2 role), own 128-B line
+#define MSA_TK_BLOCK 64      // flow kernel: pass-2 blocks, own 128-B line
 #define MSA_CPAD 256         // code segment padding (bytes) on each side of a pair's columns
 #define MSA_NCOPY 16         // byte-shifted code copies: every lane reads 16-byte aligned dwordx4
 #define MSA_CRING 1024       // single-pair LDS code ring: columns per copy (+64 B mirror), 4 copies
@@ -1397,7 +1400,7 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
 __global__ void stage_codes_kernel(const uint8_t* B, const msa_pair_desc* pairs, int n_pairs, uint8_t* cod,
                                    long long cod_copy, unsigned virt, int* ticket) {
   // the run's ticket counters and error word start at 0 (this launch precedes the DP kernel)
-  if (ticket && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 16) ticket[threadIdx.x] = 0;
+  if (ticket && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < MSA_NTICKET) ticket[threadIdx.x] = 0;
   const int p = blockIdx.y;
   if (p >= n_pairs) return;
   const msa_pair_desc pd = pairs[p];
@@ -1492,7 +1495,7 @@ __global__ __launch_bounds__(256) void chunk_add_kernel(int32_t* H, const msa_pa
     if (blockIdx.x == 0 && k == 0) {
       *skip = ok;
       if (!ok)
-        for (int t = 0; t < 16; ++t) ticket[t] = 0;
+        for (int t = 0; t < MSA_NTICKET; ++t) ticket[t] = 0;
     }
     if (ok && blockIdx.x == 0 && k == n_chunks - 1) {
       msa_stripe_meta* md = meta + pd.stripe0 + S - 1;

@@ -83,4 +83,26 @@ out = dict(tag=args.tag, workload=wl, kernel_ms=[round(x, 4) for x in kms], stri
            wait_in_ticks_mean=float(np.mean([wq[r[0] // 4, r[0] % 4, 0] for r in recs])),
            wait_cons_ticks_mean=float(np.mean([wq[r[0] // 4, r[0] % 4, 1] for r in recs])),
            ncons_mean=float(np.mean([wq[r[0] // 4, r[0] % 4, 2] for r in recs])))
+wg = full[63, 15, :, :]
+started = wg[:, 0] > 0
+if started.any():
+    ws, we, role = wg[started, 0], wg[started, 1], wg[started, 2]
+    out.update(wg_count=int(started.sum()), wg_first_start_us=round(float((ws.min() - t0) / 100.0), 2),
+               wg_last_end_us=round(float((we.max() - t0) / 100.0), 2),
+               pass1_last_end_us=round(float((we[role == 1].max() - t0) / 100.0), 2) if (role == 1).any() else None,
+               pass2_last_end_us=round(float((we[role == 2].max() - t0) / 100.0), 2) if (role == 2).any() else None,
+               wg_last_start_us=round(float((ws.max() - t0) / 100.0), 2))
+cl = full[63, 15, 2048:, :]
+claimed = cl[:, 2] > 0
+if claimed.any():
+    it0 = np.where(cl[:, 2] == 1)[0]
+    if len(it0):
+        b0 = it0[0]
+        out.update(item0_wg_start_us=round(float((wg[b0, 0] - t0) / 100.0), 2),
+                   item0_role_us=round(float((cl[b0, 0] - t0) / 100.0), 2),
+                   item0_claim_us=round(float((cl[b0, 1] - t0) / 100.0), 2),
+                   claim_us_max=round(float((cl[claimed, 1].max() - t0) / 100.0), 2))
+    io0 = full[0, 4, 0, 0]
+    if io0:
+        out.update(item0_codes_loaded_us=round(float((io0 - t0) / 100.0), 2))
 print(json.dumps(out), flush=True)
