@@ -1484,14 +1484,25 @@ __global__ __launch_bounds__(256) void chunk_add_kernel(int32_t* H, const msa_pa
   const msa_pair_desc pd = pairs[0];
   const int S = (pd.m + 63) / 64;
   __shared__ int sh_e, sh_ok;
-  if (threadIdx.x == 0) {
+  // the prefix of chunk constants and the all-converged flag, over the block's threads (a serial
+  // loop of 2 x n_chunks dependent global loads in thread 0 cost each block microseconds)
+  {
     int e = 0, ok = 1;
-    for (int j = 0; j < n_chunks; ++j) {
+    for (int j = threadIdx.x; j < n_chunks; j += blockDim.x) {
       ok &= okk[j];
       if (j <= k) e += dk[j];
     }
-    sh_e = e;
-    sh_ok = ok;
+    const int all_ok = __syncthreads_and(ok);
+    if (threadIdx.x == 0) sh_e = 0;
+    __syncthreads();
+    if (e != 0) atomicAdd(&sh_e, e);
+    __syncthreads();
+    e = sh_e;
+    ok = all_ok;
+    if (threadIdx.x == 0) sh_ok = ok;
+  }
+  if (threadIdx.x == 0) {
+    const int e = sh_e, ok = sh_ok;
     if (blockIdx.x == 0 && k == 0) {
       *skip = ok;
       if (!ok)
