@@ -127,7 +127,8 @@ def optimal_alignment_distributed(A1: bytes, B1: bytes, m: int, n: int, p: int, 
                                   group=None):
     """main_alignment_function with the partition split, over every rank of the default (or ``group``)
     process group (world size 1 without torch.distributed): returns (stdout text, stitched path), the
-    same on every rank.  ``bp`` skips the partition (optimal_alignment over a given partition)."""
+    same on every rank.  ``bp`` skips the partition (optimal_alignment over a given partition).  Each
+    rank computes on its current device (``torch.cuda.set_device(local_rank)`` first)."""
     import torch.distributed as dist
 
     A1, B1 = bytes(A1), bytes(B1)
@@ -136,17 +137,34 @@ def optimal_alignment_distributed(A1: bytes, B1: bytes, m: int, n: int, p: int, 
     world = dist.get_world_size(group) if on else 1
     part = partition_fn or gpu_partition
     solve = solve_fn or gpu_subproblem
-    box = [list(bp) if bp is not None else (part(A1, B1, m, n, p, g, h) if rank == 0 else None)]
+    box = [list(bp) if bp is not None else None]
+    if bp is None and rank == 0:
+        try:
+            box[0] = part(A1, B1, m, n, p, g, h)
+        except Exception as e:  # the other ranks must not wait on the broadcast forever
+            box[0] = RuntimeError(f"rank 0: partition failed: {e}")
     if world > 1 and bp is None:
         dist.broadcast_object_list(box, src=0, group=group)
+    if isinstance(box[0], Exception):
+        raise box[0]
     points = [tuple(int(v) for v in x) for x in box[0]]
     check_partition(points, m, n)
     order = solve_order(len(points) - 1, fix_all)
     mine = assign(order, points, world)[rank]
     # this rank's subproblems run concurrently (msa_subproblem is reentrant: each call takes its own
-    # pooled stream; ctypes drops the GIL), as msa_optimal_alignment runs them on one GPU
+    # pooled stream; ctypes drops the GIL), as msa_optimal_alignment runs them on one GPU.  libmsa
+    # works on the calling thread's current device: the workers take this rank's.
+    import torch
+
+    dev = torch.cuda.current_device() if torch.cuda.is_available() else None
+
+    def run(k):
+        if dev is not None:
+            torch.cuda.set_device(dev)
+        return solve(A1, B1, points, k, g, h)
+
     with ThreadPoolExecutor(max_workers=max(1, min(8, len(mine)))) as pool:
-        local = dict(zip(mine, pool.map(lambda k: solve(A1, B1, points, k, g, h), mine)))
+        local = dict(zip(mine, pool.map(run, mine)))
     if world > 1:
         every: List[Optional[Dict[int, List[Node]]]] = [None] * world
         dist.all_gather_object(every, local, group=group)
