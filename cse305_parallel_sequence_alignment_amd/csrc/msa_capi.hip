@@ -14,6 +14,7 @@
 #include <new>
 #include <string>
 #include <thread>
+#include <deque>
 #include <map>
 #include <tuple>
 #include <vector>
