@@ -523,7 +523,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   // run the one-pass stripe kernel
   const bool aff = kalg == MSA_ALG_SWA || kalg == MSA_ALG_REF1;
   const size_t flow_lds = (size_t)(FL_FLAGS + (FL_W + 1) * 256 * (aff ? 2 : 1)) * 4 +
-                          (size_t)(aff ? 4 : FL_NCOPY) * fl_code_bytes((int)desc->n[0]);
+                          (size_t)(aff ? 4 : FL_NCOPY) * fl_code_bytes((int)desc->n[0]) + ((aff || FL_HO != 2) ? 0 : FL_SINK);
   // affine: profile bytes score + 2e + (o - e) must be int8
   const bool aff_ok = kalg == MSA_ALG_SWA && out_mode == MSA_OUT_DIR && desc->gap_extend >= 0 &&
                       desc->gap_open >= desc->gap_extend &&

@@ -45,6 +45,7 @@ namespace msa {
 #define FL_OFF 95       // LDS code copy x, byte y <-> column y + x - FL_OFF (== CPAD-1 mod 16)
 #define FL_NCOPY 8      // byte-shifted LDS code copies (8-byte aligned 8-code reads)
 #define FL_FLAGS 128    // ints of flags at the start of LDS
+#define FL_SINK 1152    // bytes of the SW-linear hand-off sink after the code copies (FL_HO 2)
 #ifndef FL_PS
 #define FL_PS 8         // phases per pass-2 segment (pass 1 saves its state every FL_PS phases)
 #endif
@@ -59,7 +60,9 @@ namespace msa {
 #define FL_PUBLATE 0    // 1: the producer-counter read is awaited after the hand-off, with the data
 #endif
 #ifndef FL_HO
-#define FL_HO 0         // SW-linear hand-off: 0 = 16 ds_write_addtid_b32, 1 = 8 ds_write_b64
+#define FL_HO 0         // SW-linear hand-off: 0 = 16 ds_write_addtid_b32, 1 = 8 ds_write_b64 (both lane 63
+                        // alone), 2 = 4 ds_write_b128 of every lane (lanes 0..62 into a sink; measured
+                        // C2 0.478 vs 0.455 ms: the 1 KiB writes cost more LDS time than the exec switch)
 #endif
 #ifndef FL_IOSLEEP
 #define FL_IOSLEEP 1    // s_sleep of an idle io wave
@@ -193,6 +196,21 @@ __device__ __forceinline__ void ds_handoff_b64(unsigned long long m63, unsigned 
       : [sv] "=&s"(sv)
       : [m] "s"(m63), [a] "v"(addr), [x0] "v"(x0), [x1] "v"(x1), [x2] "v"(x2), [x3] "v"(x3), [x4] "v"(x4),
         [x5] "v"(x5), [x6] "v"(x6), [x7] "v"(x7), [pa] "v"(pa), [pv] "v"(pv)
+      : "memory");
+}
+
+// The same hand-off with every lane active: no exec switch, so no SALU exec writes and no
+// wait states before the next DPP.  Lane 63 writes its 16 values as four b128 to the ring
+// block (wa) and the counter (pa); lanes 0..62 write the same-shaped data to the shared sink
+// (wa = sink + 16 lane, pa = sink + 4 lane: consecutive lanes, no bank conflicts), which
+// nothing reads.  5 DS ops instead of 17.
+__device__ __forceinline__ void ds_handoff_all(unsigned wa, const fl_v4i (&x)[4], unsigned pa, int pv) {
+  asm volatile(
+      "ds_write_b128 %[a], %[x0]\n\tds_write_b128 %[a], %[x1] offset:16\n\t"
+      "ds_write_b128 %[a], %[x2] offset:32\n\tds_write_b128 %[a], %[x3] offset:48\n\t"
+      "ds_write_b32 %[pa], %[pv]"
+      :
+      : [a] "v"(wa), [x0] "v"(x[0]), [x1] "v"(x[1]), [x2] "v"(x[2]), [x3] "v"(x[3]), [pa] "v"(pa), [pv] "v"(pv)
       : "memory");
 }
 
@@ -881,6 +899,12 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
       const unsigned a_cons2 = lds_addr(flags + 64 + w + 1);
       const bool two_cons = SAVE || (w + 1 == W);
       const unsigned a_dummy = lds_addr(flags + 96 + 8 * (w & 1));  // sink for a phase with nothing to hand off
+#if FL_HO == 2
+      // every-lane hand-off: lanes 0..62 (and lane 63 with nothing to hand off) write to the
+      // sink after the code copies (FL_SINK bytes, shared by the compute waves, never read)
+      const unsigned a_sink = lds_addr(codes + FL_NCOPY * L8) + 16u * (unsigned)lane;
+      const unsigned a_pa = (lane == 63) ? a_prog_me : lds_addr(codes + FL_NCOPY * L8) + 4u * (unsigned)lane;
+#endif
       unsigned plo, phi, plo2 = 0, phi2 = 0;
       fl_profile<GS, FLOOR>(kp.match, kp.mismatch, g, ac, plo, phi);
       if constexpr (R == 2) fl_profile<GS, FLOOR>(kp.match, kp.mismatch, g, ac2, plo2, phi2);
@@ -1011,7 +1035,14 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
             if constexpr (R == 2) gstore(sp + 128, ((unsigned long long)ep << 32) | (unsigned)X2);
           }
         }
-        int hv[16], xo[16];
+        int hv[16];
+#if FL_HO == 2
+        fl_v4i xo4[4];
+#define FL_XO(kx_) xo4[(kx_) >> 2][(kx_) & 3]
+#else
+        int xo[16];
+#define FL_XO(kx_) xo[kx_]
+#endif
         int pubn = 0;
         const int negct = negct0 - 16 * g * q;
 #pragma unroll
@@ -1025,7 +1056,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
             const int s = ((int)(s4 << (24 - 8 * kk))) >> 24;
             if constexpr (R == 1) {
               const int h = fl_step<GS, FLOOR>(IN[kx >> 2][kx & 3], s, X, U, g);
-              xo[kx] = X;
+              FL_XO(kx) = X;
               if constexpr (BEST) hv[kx] = GS ? h + negct + gk[kx] : h;
             } else {
               // row 1's up = the previous lane's row 2 (lane 0: the producer's value);
@@ -1042,7 +1073,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
               if constexpr (FLOOR) h2 = imax(h2, 0);
               asm("" : "+v"(h2));
               X2 = GS ? h2 : h2 - g;
-              xo[kx] = X2;
+              FL_XO(kx) = X2;
             }
           }
         }
@@ -1060,11 +1091,14 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         if (__builtin_expect((MSA_ABL & 80) == 0 && wr && consv < bq - (FL_RINGB - 1), 0))
           refresh_cons(bq - (FL_RINGB - 1));
         const unsigned wa = wr ? a_ring_out + (unsigned)((bq & (FL_RINGB - 1)) * 64) : a_dummy;
-#if FL_HO == 1
+#if FL_HO == 2
+        ds_handoff_all((lane == 63 && wr) ? wa : a_sink, xo4, a_pa, q + 1);
+#elif FL_HO == 1
         ds_handoff_b64(m63, wa, xo, a_prog_me, q + 1);
 #else
         ds_handoff_tid(m63, wa - 252u, xo, a_prog_me, q + 1);  // (-6.5% on C2 vs four single-lane b128 writes)
 #endif
+#undef FL_XO
 #ifdef MSA_STAMPS
         if (q == dq) FL_STAMP(0, 3, __builtin_amdgcn_s_memrealtime());
 #endif
