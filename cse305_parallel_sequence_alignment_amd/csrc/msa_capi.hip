@@ -718,7 +718,8 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
 // 0.768, (16, 16) 0.733, (20, 10) 0.678 -- and (16, 8) did not converge in every chunk (the
 // exact fallback ran: 18.3 ms).  C3's pair converges within ~900 rows, its synthetic mutated
 // copy within ~1,024; 20 stripes = 1,280 rows.  Chunk workgroups of 4 or 12 waves instead of 8:
-// 0.90 and 0.72 ms (8: 0.67).
+// 0.90 and 0.72 ms (8: 0.67).  (20, 6) = 254 chunks, one per CU: not every chunk converged
+// (17.4 ms with the fallback) -- more start rows, and the slowest needs more than 1,280 rows.
 #ifndef MSA_CHUNK_WARM
 #define MSA_CHUNK_WARM 20  // warm-up stripes
 #endif
