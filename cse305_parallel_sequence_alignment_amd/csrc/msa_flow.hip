@@ -39,7 +39,9 @@
 namespace msa {
 
 #ifndef FL_W
-#define FL_W 4          // compute waves per workgroup: one per SIMD
+#define FL_W 4          // compute waves per workgroup: one per SIMD (8, two per SIMD, measured: C2
+                        // 0.576 vs 0.455 ms, C5 2.78 vs 1.91, ref 1.73 vs 1.12 -- a chain wave keeps its
+                        // SIMD's issue busy, so a second wave on it slows both)
 #endif
 #define FL_RINGB 16     // ring blocks of 16 columns per link (256 columns)
 #define FL_OFF 95       // LDS code copy x, byte y <-> column y + x - FL_OFF (== CPAD-1 mod 16)
