@@ -255,12 +255,13 @@ int kernel_shape(kfn_t fn, int threads, size_t lds) {
 // single-pair phase length: 32 steps for one carried value (SW linear); 16 when
 // two or three values per cell are carried (register pressure: no spills)
 constexpr int ks_single(int alg) { return (alg == MSA_ALG_SWL || alg == MSA_ALG_SWL0) ? MSA_KS_SINGLE : 16; }
+constexpr int ks_batch(int alg) { return (alg == MSA_ALG_SWLP) ? MSA_KS_BATCH_SWLP : MSA_KS_BATCH; }
 
 template <int ALG, int OUT, int TP>
 kfn_t kf(bool sgl) {
   // single pair: (MSA_WAVES_SINGLE waves, MSA_KS_SINGLE steps/phase); batch: (MSA_WAVES_BATCH, MSA_KS_BATCH)
   return sgl ? stripe_kernel<ALG, OUT, TP, MSA_WAVES_SINGLE, ks_single(ALG), true>
-                               : stripe_kernel<ALG, OUT, TP, MSA_WAVES_BATCH, MSA_KS_BATCH, false>;
+                               : stripe_kernel<ALG, OUT, TP, MSA_WAVES_BATCH, ks_batch(ALG), false>;
 }
 
 kfn_t pick_kernel(int alg, int out, int tp, bool sgl) {
@@ -540,7 +541,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   P->flow2 = flow && (out_mode == MSA_OUT_H || aff);
   const int W = flow ? FL_W : (single ? MSA_WAVES_SINGLE : MSA_WAVES_BATCH);
   P->W = W;
-  const int KS = flow ? 16 : (single ? ks_single(kalg) : MSA_KS_BATCH);
+  const int KS = flow ? 16 : (single ? ks_single(kalg) : ks_batch(kalg));
   P->KS = KS;
   P->threads = (flow ? W + 2 : W + 1 + (single ? 1 : 0)) * 64;
   // rows per lane of the flow kernel (two-pass plans): 2 halves the inter-wave hand-offs per row
@@ -918,6 +919,8 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
   if (P->chunked) {
     // verify every chunk's constant, add the prefix of the constants to its cells; then the
     // exact single-mode launch, which returns at once when *skip == 1
+    // (a fused check + add launch, roles by arrival ticket, the adders' first loads in flight
+    // across the checks, measured slower: C3 0.94 vs 0.67 ms)
     hipLaunchKernelGGL(chunk_check_kernel, dim3(P->n_chunks), dim3(256), 0, st, (const int*)P->d_ck, P->ckw, P->d_dk,
                        P->d_okk);
     HIPCHK(hipGetLastError());
