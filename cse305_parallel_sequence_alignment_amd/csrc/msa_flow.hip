@@ -514,7 +514,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
             valf[r] = MSA_NEG;
             if constexpr (GOT) {  // row 0, tagged and shifted (oe = h)
               val[r] = col < 0 ? MSA_NEG : (col == 0 ? 3 : 2 - 4 * oe);
-              valf[r] = col < 0 ? MSA_NEG : (col == 0 ? 3 - 4 * oe : 2 - 8 * oe);
+              valf[r] = col < 0 ? MSA_NEG : (col == 0 ? 3 : 2 - 4 * oe);  // D~ + 4h (pass-1 convention)
             }
           }
           nb = min(16, Bmax - b + 1);
@@ -598,9 +598,9 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
             const int vf = AFF ? *(const lds_int*)(rings + l * 256 * NV + 256 + (blk & (FL_RINGB - 1)) * 16 + c) : 0;
             if (SAVE && (MSA_ABL & 4) == 0) {
               gstore(a.br + (size_t)(kc - 1) * a.brw + 16 * blk + c, ((unsigned long long)ep << 32) | (unsigned)v);
-              if constexpr (AFF)
+              if constexpr (AFF)  // (Gotoh: D~ + 4h on the links, D~ for pass 2)
                 gstore(a.br + (size_t)(S_br + kc - 1) * a.brw + 16 * blk + c,
-                       ((unsigned long long)ep << 32) | (unsigned)vf);
+                       ((unsigned long long)ep << 32) | (unsigned)(GOT ? vf - 4 * oe : vf));
             }
             if (l == W) {
               const int col = fl_cs(kc) + 16 * blk + c;
@@ -658,10 +658,10 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
       int U = Zl - g;
       int E = MSA_NEG, Fo = MSA_NEG;
       const int tmin = 1 - cs + lane;  // Gotoh: the lane's first step at column >= 1
-      if constexpr (GOT) {
+      if constexpr (GOT) {  // (E / Fo carry R~ + 4h / D~ + 4h in pass 1: see the step)
         Zl = 1 - 4 * oe;
-        E = 1 - 8 * oe;
-        Fo = 1 - 4 * oe;
+        E = 1 - 4 * oe;
+        Fo = 1;
         U = MSA_NEG;
       }
       int pubv = 0, consv = 0;
@@ -751,8 +751,8 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         if (q % FL_PS == 0) {  // pass 2 restarts here: each lane's (Z left, E~, F~, diagonal Z)
           unsigned long long* sp = a.snap + ((size_t)k * a.nseg + q / FL_PS) * 256 + lane;
           gstore(sp, ((unsigned long long)ep << 32) | (unsigned)Zl);
-          gstore(sp + 64, ((unsigned long long)ep << 32) | (unsigned)E);
-          gstore(sp + 128, ((unsigned long long)ep << 32) | (unsigned)Fo);
+          gstore(sp + 64, ((unsigned long long)ep << 32) | (unsigned)(GOT ? E - 4 * oe : E));  // pass 2: R~, D~
+          gstore(sp + 128, ((unsigned long long)ep << 32) | (unsigned)(GOT ? Fo - 4 * oe : Fo));
           gstore(sp + 192, ((unsigned long long)ep << 32) | (unsigned)U);
         }
         int xz[16], xf[16];
@@ -768,21 +768,26 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
             if (kx == FL_PF) issue_reads(q + 1, Zn, Fn, Cln, Chn, pubn);
             const int sc = ((int)(s4 << (24 - 8 * kk))) >> 24;
             if constexpr (GOT) {
+              // R~ and D~ are carried + 4h (E = R~ + 4h, Fo / F = D~ + 4h): then
+              //   R~ + 4h = max3(t1, t2 + 4h, t3),  D~ + 4h = max3(t1, t2, t3 + 4h)
+              // and t2 = t2' - 4h, t3 = t3' - 4h (4h keeps the tag bits): 11 VALU per step, not 12.
+              // SNAP and io-out's BR copy hand pass 2 the unshifted values; granules and rings keep
+              // this convention.
               const int uH = dpp_shr1(Z[kx >> 2][kx & 3], Zl);
               const int uD = dpp_shr1(F[kx >> 2][kx & 3], Fo);
               const int t1 = (int)((unsigned)U | 3u) + sc;
-              const int t2 = (int)(((unsigned)E & ~3u) | 2u);
-              const int t3 = (int)(((unsigned)uD & ~3u) | 1u);
-              const int t1h = t1 - 4 * oe;
+              const int t2p = (int)(((unsigned)E & ~3u) | 2u);
+              const int t3p = (int)(((unsigned)uD & ~3u) | 1u);
+              const int t2 = t2p - 4 * oe, t3 = t3p - 4 * oe;
               int h = imax3(t1, t2, t3);
-              int rr = imax3(t1h, t2, t3 - 4 * oe);
-              int dd = imax3(t1h, t2 - 4 * oe, t3);
+              int rr = imax3(t1, t2p, t3);
+              int dd = imax3(t1, t2, t3p);
               asm("" : "+v"(h));
               if constexpr (HEAD) {
                 const bool before = 16 * q + kx < tmin;
                 h = before ? 1 - 4 * oe : h;
-                rr = before ? 1 - 8 * oe : rr;
-                dd = before ? 1 - 4 * oe : dd;
+                rr = before ? 1 - 4 * oe : rr;
+                dd = before ? 1 : dd;
               }
               U = uH;
               Zl = h;
