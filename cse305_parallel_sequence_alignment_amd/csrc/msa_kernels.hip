@@ -1453,12 +1453,13 @@ __global__ __launch_bounds__(256) void chunk_check_kernel(const int* __restrict_
   if (threadIdx.x == 0) { first = 0x7fffffff; bad = 0; }
   __syncthreads();
   constexpr int NH = MSA_NEG / 2;
-  int mybad = 0;
+  int mybad = 0, myfirst = 0x7fffffff;  // (one LDS atomic per thread, not per finite entry)
   for (int e = threadIdx.x; e < 2 * ckw; e += 256) {
     const int x = end[e], y = warm[e];
     if ((x > NH) != (y > NH)) mybad = 1;
-    else if (x > NH) atomicMin(&first, e);
+    else if (x > NH && myfirst == 0x7fffffff) myfirst = e;  // e grows: the thread's first is its least
   }
+  if (myfirst != 0x7fffffff) atomicMin(&first, myfirst);
   if (mybad) atomicOr(&bad, 1);
   __syncthreads();
   const int f = first;
