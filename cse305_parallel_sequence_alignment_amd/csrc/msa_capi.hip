@@ -903,7 +903,11 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
   {
     const unsigned virt = (P->kp.alg == MSA_ALG_SWL || P->kp.alg == MSA_ALG_SWL0 || P->kp.alg == MSA_ALG_SWLP ||
                            P->kp.alg == MSA_ALG_SWA) ? MSA_VIRT_CODE : 0u;
-    hipLaunchKernelGGL(stage_codes_kernel, dim3(64, (unsigned)P->segs.size()), dim3(256), 0, st, dB, P->d_segs,
+    // about two output words per thread for one long pair (64 x 256 threads took 22 us for
+    // C3's 97k columns, 24 dependent rounds each), at least 64 workgroups per segment
+    const int64_t words = MSA_NCOPY * (P->cod_copy / 4) / std::max<int64_t>(1, (int64_t)P->segs.size());
+    const unsigned gx = (unsigned)std::min<int64_t>(1024, std::max<int64_t>(64, words / 512));
+    hipLaunchKernelGGL(stage_codes_kernel, dim3(gx, (unsigned)P->segs.size()), dim3(256), 0, st, dB, P->d_segs,
                        (int)P->segs.size(), P->d_cod, (long long)P->cod_copy, virt, P->d_ticket);
     HIPCHK(hipGetLastError());
   }
