@@ -2,6 +2,7 @@
 """Benchmark of the hot path (BASELINE.json metric: GCUPS, 10k x 10k Smith-Waterman).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c4|c3|c5|ref] [--ref-len L]
+                    [--ref-pair a,b]
 
 One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI when
 launched by torch.distributed.run).  A "step" is one pass of the DP fill over
@@ -19,7 +20,8 @@ one batch of input already resident in HBM:
   traceback on the device (one wave walks the bits from the end cell): a step
   is fill + traceback.
 * ref: the reference's own boundary, main_alignment_function (global Gotoh,
-  g=1 h=2, start/end type -1) on seq0 x seq1 at --ref-len (10k default, 20k):
+  g=1 h=2, start/end type -1) on seq a x seq b (--ref-pair, default 0,1) at --ref-len (10k default;
+  0 = the whole sequences, as the reference's own callers pass them, testing.cpp:261,345):
   a step is the fill writing 1 B/cell direction bytes + find_alignment's walk
   on the device, inputs resident in HBM.  The whole C-ABI call (host buffers
   in, printed text out: PCIe, plan set-up, node list and print_seq included)
@@ -62,7 +64,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c2", choices=["c2", "c4", "c3", "c5", "ref"])
-    ap.add_argument("--ref-len", type=int, default=10000, help="ref workload: seq0 x seq1 prefix length")
+    ap.add_argument("--ref-len", type=int, default=10000,
+                    help="ref workload: prefix length of both sequences (0 = whole sequences)")
+    ap.add_argument("--ref-pair", default="0,1", help="ref workload: dataset indices a,b of the pair")
     ap.add_argument("--pairs", type=int, default=0,
                     help="c4: run only the first PAIRS of the 1024 pairs (e.g. 128 = one rank's share at N=8)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -70,7 +74,7 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(wl: str, A: bytes, B: bytes, cores: int):
+def cpu_baseline(wl: str, A: bytes, B: bytes, cores: int, pairs=None):
     """The reference's CPU method (row sweep, fresh std::threads per row phase, prefix-max
     horizontal gap: oracle/cpu_rowsweep.cpp) on this host, p' = 1 and p' = cores, bounded samples.
     c3: the reference's full tables cannot hold a 97k x 97k pair, so its baseline is
@@ -88,6 +92,26 @@ def cpu_baseline(wl: str, A: bytes, B: bytes, cores: int):
                            f"thread) over the whole {len(A)} x {len(B)} band, {secs:.2f} s; host nproc "
                            f"{os.cpu_count()}",
                     points=[dict(threads=1, rows=len(A), cols=len(B), seconds=round(secs, 3))])
+
+    if wl == "c4" and pairs:
+        # the reference's pair-level fan-out (testing.cpp:269-280: one std::thread per pair, each calling
+        # main_alignment_function): whole 4,000 x 4,000 pairs, p' = 1 each, `cores` at a time
+        from concurrent.futures import ThreadPoolExecutor
+
+        sample = pairs[:8 * cores]
+        O.rowsweep(sample[0][:200], B[:200], p=1, mode=1)  # load the library outside the timed region
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(max_workers=cores) as ex:  # (ctypes releases the GIL during each call)
+            list(ex.map(lambda q: O.rowsweep(q, B, p=1, mode=1, g=1.0, match=1, mismatch=0), sample))
+        secs = time.perf_counter() - t0
+        cells = sum(len(q) * len(B) for q in sample)
+        return dict(value=round(cells / secs / 1e9, 4), unit="GCUPS", cores=cores, kind="port",
+                    sample=f"the reference's pair-level fan-out (testing.cpp:269-280, one thread per pair) over "
+                           f"the first {len(sample)} of this rank's C4 pairs, whole {len(sample[0])} x {len(B)} "
+                           f"pairs, each the reference's row-sweep method at p'=1 (oracle/cpu_rowsweep.cpp, "
+                           f"SW-linear int32), {cores} pairs at a time on {cores} threads, {secs:.2f} s; host "
+                           f"nproc {os.cpu_count()}, this job's CPU share {cores}",
+                    points=[dict(threads=cores, pairs=len(sample), seconds=round(secs, 3))])
 
     # c3 / c5 / ref (affine gaps): the reference's own Gotoh recurrence; c2 / c4: SW linear int32
     mode = 0 if wl in ("c3", "c5", "ref") else 1
@@ -137,17 +161,41 @@ def load_traffic(wl: str):
     return None
 
 
+def launch_ranks(gpus: int) -> int:
+    """``bench.py --gpus N`` started without a launcher: run the same command under torch.distributed.run
+    (N ranks, one per GPU) as a CHILD process -- nothing in this process has touched the GPU, and it never
+    replaces itself (no exec) -- and return the child's exit code.  Rank 0's JSON line reaches stdout through
+    the inherited descriptor."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve())] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but the launcher started {world} rank(s) (WORLD_SIZE)")
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"RCCL sees {dist.get_world_size()} ranks, --gpus {args.gpus}")
     dev = torch.device("cuda", local)
     from cse305_parallel_sequence_alignment_amd import _lib as LB
     from cse305_parallel_sequence_alignment_amd import data
@@ -183,13 +231,16 @@ def main():
                 "device (ops + begin cell)")
     elif wl == "ref":
         L = args.ref_len
-        A, B = data.bundled()[0][:L], data.bundled()[1][:L]
+        ia, ib = (int(x) for x in args.ref_pair.split(","))
+        A, B = data.bundled()[ia], data.bundled()[ib]
+        if L > 0:
+            A, B = A[:L], B[:L]
         m, n = len(A), len(B)
         pairs_m, pairs_n, a_off, b_off = [m], [n], [0], [0]
         plan_kw = dict(alg=LB.REF_GOTOH, cells=LB.CELLS_DIR, match=1, mismatch=0, gap_open=3, gap_extend=1,
                        start_type=-1)
         cells_per_step = m * n
-        desc = (f"main_alignment_function's path: reference Gotoh {m}x{n} (seq0 x seq1, g=1 h=2, start/end type -1), "
+        desc = (f"main_alignment_function's path: reference Gotoh {m}x{n} (seq{ia} x seq{ib}{'' if L > 0 else ', whole'}, g=1 h=2, start/end type -1), "
                 f"1 B/cell direction bytes + find_alignment's walk on the device")
     else:  # c4
         total = args.pairs if args.pairs > 0 else data.C4_PAIRS
@@ -303,8 +354,12 @@ def main():
         from cse305_parallel_sequence_alignment_amd import api
 
         inf = tb_info.cpu().tolist()
+        # the reference's own outputs at this size (make_golden.py at_size), else the 1 B/cell oracle's
+        # whole-sequence fixtures (make_whole.py), else the 1 B/cell oracle itself (bounded)
         fx = [c for c in json.loads((REPO / "tests" / "golden" / "at_size.json").read_text())
-              if (c["a"], c["b"], c["L"], c["g"], c["h"]) == (0, 1, m, 1.0, 2.0)]
+              if (c["a"], c["b"], c["L"], c["g"], c["h"]) == (ia, ib, m, 1.0, 2.0) and m == n]
+        fxw = [c for c in json.loads((REPO / "tests" / "golden" / "whole.json").read_text())
+               if (c["a"], c["b"], c["m"], c["n"]) == (ia, ib, m, n)]
         # the boundary call itself (host buffers in, text out), timed outside the device-resident steps,
         # after one untimed call (its first call in this process fills the device-block pool)
         api.main_alignment_text(b"\0" + A, b"\0" + B, m, n, 32, 1.0, 2.0)
@@ -319,8 +374,13 @@ def main():
             checks["text_matches_reference"] = bool(
                 hashlib.md5((lines[0] + "\n" + lines[1] + "\n").encode()).hexdigest() == fx[0]["lines_md5"] and
                 len(lines[0]) == fx[0]["n_nodes"] == inf[0])
-        else:
-            o = O.main_alignment_text(A, B, 1.0, 2.0)
+        elif fxw:
+            checks["score_matches_cpu"] = bool(sc == fxw[0]["score"] == max(res[0]["fin"]))
+            checks["text_matches_cpu"] = bool(
+                hashlib.md5(text.encode("latin-1")).hexdigest() == fxw[0]["text_md5"] and
+                len(lines[0]) == fxw[0]["n_nodes"] == inf[0])
+        elif m * n <= 2.5e9:
+            o = O.main_alignment_text_dir(A, B, 1, 2)
             checks["text_matches_cpu"] = bool(text == o[0])
     else:
         # the score all-gather's share of a step (outside the timed region): the collective alone, on
@@ -393,14 +453,17 @@ def main():
         cpu = None
         if not args.no_cpu_baseline:
             try:
-                cpu = cpu_baseline(wl, A[:data.C4_LEN] if wl == "c4" else A, B, min(16, os.cpu_count() or 1))
+                # the job's CPU share: 16 host threads per GPU on this pool (the box's nproc counts the whole
+                # machine); the line states both
+                cpu = cpu_baseline(wl, A[:data.C4_LEN] if wl == "c4" else A, B, min(16, os.cpu_count() or 1),
+                                   pairs=qs if wl == "c4" else None)
             except Exception as e:  # pragma: no cover
                 cpu = dict(value=None, unit="GCUPS", cores=1, kind="port", sample=f"failed: {e}")
         line = {
             "metric": "GCUPS (DP cell updates/s) + max-score match vs CPU, 10k×10k SW",
             "value": round(gcups, 3),
             "unit": "GCUPS",
-            "n_gpus": world,
+            "n_gpus": dist.get_world_size() if world > 1 else 1,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),

@@ -67,6 +67,9 @@ int current_device() {
   return dev;
 }
 
+// Frees pooled blocks held by idle cached plans (msa_refapi.inc) when the device runs out.
+void (*g_pool_reclaim)() = nullptr;
+
 // Device memory pool.  The reference's harness calls main_alignment_function
 // from hardware_concurrency threads at once (testing.cpp:145-158, 269-280,
 // 352-358); with plain hipMalloc/hipFree every call would serialize on
@@ -104,8 +107,10 @@ class DevPool {
     }
     void* p = nullptr;
     if (hipMalloc(&p, c) != hipSuccess) {
-      // cached blocks of other sizes may be what fills the device: release them, retry once
+      // cached blocks of other sizes (and those idle cached plans hold) may be what fills the
+      // device: release them, retry once
       (void)hipGetLastError();
+      if (g_pool_reclaim) g_pool_reclaim();
       release(dev);
       p = nullptr;
       if (hipMalloc(&p, c) != hipSuccess) {
@@ -518,13 +523,22 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   // link through the LDS row buffer) beats a chain of cross-workgroup hand-offs.
   const bool single = desc->single != 0;
   P->d.single = single ? 1 : 0;
-  // flow kernels: one SW-linear pair whose 8 LDS code copies fit next to the rings
-  // (n <= ~19.5k columns), or one SW-affine / reference-Gotoh (start type -1, tagged) pair
-  // with direction bytes (two values per link column, 4 code copies: n <= ~37k); wider pairs
-  // run the one-pass stripe kernel
+  // flow kernels: one SW-linear pair (8 byte-shifted LDS code rings), or one SW-affine /
+  // reference-Gotoh (start type -1, tagged) pair with direction bytes (two values per link
+  // column, 4 code rings); the column codes stream through fixed-size LDS rings, so any n fits
   const bool aff = kalg == MSA_ALG_SWA || kalg == MSA_ALG_REF1;
-  const size_t flow_lds = (size_t)(FL_FLAGS + (FL_W + 1) * 256 * (aff ? 2 : 1)) * 4 +
-                          (size_t)(aff ? 4 : FL_NCOPY) * fl_code_bytes((int)desc->n[0]) + ((aff || FL_HO != 2) ? 0 : FL_SINK);
+  size_t flow_lds = (size_t)(FL_FLAGS + (FL_W + 1) * 256 * (aff ? 2 : 1)) * 4 +
+                    (size_t)(aff ? 4 : FL_NCOPY) * FL_CSTR + ((aff || FL_HO != 2) ? 0 : FL_SINK);
+  // One flow workgroup per CU: a pass-2 workgroup sharing a CU with a pass-1 one would take issue
+  // slots from its chain waves (one chain wave keeps its SIMD's issue busy most of each step,
+  // DESIGN §5).  MSA_FLOW_LDS_MIN (bytes, diagnostic) overrides the floor.
+  {
+    static const long lds_min = [] {
+      const char* e = std::getenv("MSA_FLOW_LDS_MIN");
+      return e ? std::strtol(e, nullptr, 10) : 80 * 1024 + 1024;
+    }();
+    flow_lds = std::max(flow_lds, (size_t)std::max(0L, lds_min));
+  }
   // affine: profile bytes score + 2e + (o - e) must be int8
   const bool aff_ok = kalg == MSA_ALG_SWA && out_mode == MSA_OUT_DIR && desc->gap_extend >= 0 &&
                       desc->gap_open >= desc->gap_extend &&

@@ -48,6 +48,13 @@ namespace msa {
 #define FL_NCOPY 8      // byte-shifted LDS code copies (8-byte aligned 8-code reads)
 #define FL_FLAGS 128    // ints of flags at the start of LDS
 #define FL_SINK 1152    // bytes of the SW-linear hand-off sink after the code copies (FL_HO 2)
+// Column codes stream through an LDS ring per copy: copy-local byte y sits at y mod FL_CRING,
+// and the 16 bytes at ring position 0 are mirrored past the end (FL_CSTR = ring + guard), so
+// every 16-byte read at any ring position is contiguous.  io-in refills a slot once every
+// compute wave has passed it, so the kernel runs any n (whole-row copies capped SW linear at
+// n <= ~19.5k and affine / Gotoh at ~37k).
+#define FL_CRING 4096
+#define FL_CSTR (FL_CRING + 16)
 #ifndef FL_PS
 #define FL_PS 8         // phases per pass-2 segment (pass 1 saves its state every FL_PS phases)
 #endif
@@ -376,15 +383,15 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
   // taken); dummy sink 96..127
   int* flags = smem;
   int* rings = smem + FL_FLAGS;                                               // [W+1 links][NV][256]
-  uint8_t* codes = reinterpret_cast<uint8_t*>(rings + (W + 1) * 256 * NV);  // [NCP][L8]
-  const int L8 = kp.lds_code_bytes;
+  uint8_t* codes = reinterpret_cast<uint8_t*>(rings + (W + 1) * 256 * NV);  // [NCP][FL_CSTR] rings
+  const int L8 = kp.lds_code_bytes;  // bytes of a copy's whole (linear) code row
   const msa_pair_desc pd = a.pairs[0];
   const int m = pd.m, n = pd.n;
   const int S = (m + 64 * R - 1) / (64 * R);
   const int g = kp.gap_ext;
   const int oe = kp.gap_open - kp.gap_ext;  // affine
   const unsigned ep = kp.epoch;
-  const int grp = (int)(blockIdx.x & 7), chunk = kp.sched_cap;
+  const int chunk = kp.sched_cap;
 
 #ifdef MSA_STAMPS
   // workgroup lifetimes: item 63 / wave 15's area, q = blockIdx.x: slot 0 start, 1 end, 2 role
@@ -394,19 +401,26 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
   };
   wg_stamp(0, __builtin_amdgcn_s_memrealtime());
 #endif
+  // Role by arrival, not by blockIdx: the first nflow workgroups to START run pass 1,
+  // the later ones pass-2 blocks.  A pass-2 block waits only on pass-1 outputs, and
+  // every pass-1 role is held by a workgroup that is already running (and stays
+  // resident until every item is claimed), so progress does not depend on the order
+  // in which the hardware dispatches workgroups, or on CUs held by other kernels.
+  if (threadIdx.x == 0) smem[1] = atomicAdd(a.ticket + MSA_TK_ARRIVE, 1);
+  __syncthreads();
+  const int arrival = uni(smem[1]);
+  // Pass-1 items come from 8 chunks, a workgroup's own chunk first: blockIdx & 7 (round-robin
+  // placement puts workgroup b on XCD b % 8, so a chunk's consecutive items share an L2),
+  // except that the first 8 arrivals take chunk = arrival: every chunk's first item is then
+  // claimed by a running workgroup even if the workgroup with blockIdx c is not resident (CUs
+  // held by other launches), and a chunk's later items wait only on claimed ones.
+  const int grp = arrival < 8 ? arrival : (int)(blockIdx.x & 7);
   if constexpr (SAVE) {
-    // Role by arrival, not by blockIdx: the first nflow workgroups to START run pass 1,
-    // the later ones pass-2 blocks.  A pass-2 block waits only on pass-1 outputs, and
-    // every pass-1 role is held by a workgroup that is already running (and stays
-    // resident until every item is claimed), so progress does not depend on the order
-    // in which the hardware dispatches workgroups, or on CUs held by other kernels.
-    if (threadIdx.x == 0) smem[1] = atomicAdd(a.ticket + MSA_TK_ARRIVE, 1);
-    __syncthreads();
 #ifdef MSA_STAMPS
     if (a.stamps && threadIdx.x == 0 && blockIdx.x < 2048)
       a.stamps[(((size_t)63 * 16 + 15) * 4096 + 2048 + blockIdx.x) * 4 + 0] = __builtin_amdgcn_s_memrealtime();
 #endif
-    if (uni(smem[1]) >= a.nflow) {
+    if (arrival >= a.nflow) {
 #ifdef MSA_STAMPS
       wg_stamp(2, 2);
 #endif
@@ -471,9 +485,24 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
       const int Pc = fl_P(k0, m, n, R);
       const int Bmax = (k0 == 0) ? Pc - 1 : min(Pc - 1, fl_bmax(k0, m, n, R));
       const uint8_t* gcod = a.cod + pd.cod_off;
-      int Yr = 0;  // bytes [0, Yr) of every LDS code copy are loaded
+      int Yr = 0;  // bytes [0, Yr) of every copy's code row have been loaded into the rings
+      const int nact = min(W, S - k0);  // compute waves with a stripe in this item
+      // Ring slots are free below byte 16 c + FL_CRING - 32 of every copy, c = the slowest active
+      // compute wave's finished phases: a wave past phase c - 1 reads (phase >= c) bytes >= cs -
+      // 63 + FL_OFF - 7 + 16 c >= 16 c + 10, and loading chunk y overwrites chunk y - FL_CRING
+      // (and, at ring position 0, the guard that mirrors it).
+      auto code_cap = [&]() __attribute__((always_inline)) {
+        int c = 1 << 30;
+#pragma unroll
+        for (int w2 = 0; w2 < W; ++w2)
+          if (w2 < nact) c = min(c, lds_vload(flags + 33 + w2));
+        FL_CBAR();
+        return 16 * uni(c) + FL_CRING - 32;
+      };
       auto load_codes = [&](int Y1) __attribute__((always_inline)) {
         Y1 = min(Y1, L8);
+        if (Y1 <= Yr) return;
+        Y1 = min(Y1, code_cap());
         const int tot = NCP * ((Y1 - Yr) / 16);  // 16-byte chunks over all copies
         for (int c0 = 0; c0 < tot; c0 += 4 * 64) {     // 4 loads in flight per lane
           int4 v[4];
@@ -487,7 +516,12 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
           for (int r = 0; r < 4; ++r) {
             const int c = c0 + r * 64 + lane;
             const int x = c & (NCP - 1), y = Yr + 16 * (c / NCP);
-            if (c < tot) *(lds_int4*)(codes + x * L8 + y) = fl_v4i{v[r].x, v[r].y, v[r].z, v[r].w};
+            const int pos = y & (FL_CRING - 1);
+            const fl_v4i d{v[r].x, v[r].y, v[r].z, v[r].w};
+            if (c < tot) {
+              *(lds_int4*)(codes + x * FL_CSTR + pos) = d;
+              if (pos == 0) *(lds_int4*)(codes + x * FL_CSTR + FL_CRING) = d;  // the guard
+            }
           }
         }
         Yr = max(Yr, Y1);
@@ -554,8 +588,17 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
           if (++spins > FL_SPIN_MAX) { if (lane == 0) atomicExch(a.err, 10); break; }
           continue;
         }
-        // codes for the blocks' next phases must be in LDS before they are published
-        if (Yr < L8 && Yr < 16 * (b + nb) + 192) load_codes(16 * (b + nb) + 1024);
+        // codes for the blocks' next phases must be in LDS before they are published (a full
+        // code ring -- the last compute wave far behind -- holds the blocks back)
+        if (Yr < L8 && Yr < 16 * (b + nb) + 192) {
+          load_codes(16 * (b + nb) + 1024);
+          if (Yr < L8) nb = min(nb, (Yr - 192) / 16 - b);
+          if (nb <= 0) {
+            __builtin_amdgcn_s_sleep(FL_IOSLEEP);
+            if (++spins > FL_SPIN_MAX) { if (lane == 0) atomicExch(a.err, 10); break; }
+            continue;
+          }
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int blk = b + 4 * r + (lane >> 4);
@@ -645,11 +688,13 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
       unsigned plo, phi;
       if constexpr (GOT) fl_profile_got(g, ac, plo, phi);
       else fl_profile_aff(kp.match, kp.mismatch, g, oe, ac, plo, phi);
-      unsigned a_code;
+      // LDS code address of phase q: ring of copy x, byte (y_lane + 16 q) mod FL_CRING
+      unsigned a_cring, y_code;
       {
         const int c0 = cs - lane + FL_OFF;
         const int x = c0 & (NCP - 1);
-        a_code = lds_addr(reinterpret_cast<int*>(codes + x * L8 + (c0 - x)));
+        a_cring = lds_addr(reinterpret_cast<int*>(codes + x * FL_CSTR));
+        y_code = (unsigned)(c0 - x);
       }
       // step 0: lane r at column cs - r (virtual, H = 0): its left cell's Z, the diagonal Z
       // (Gotoh: Zl / E / Fo / U hold H~ / R~ / D~ / diagonal H~, the column-0 border)
@@ -681,7 +726,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         F[1] = ds_read_b128<1040>(ra);
         F[2] = ds_read_b128<1056>(ra);
         F[3] = ds_read_b128<1072>(ra);
-        ds_read_codes16(a_code + 16 * q, Cl, Ch);
+        ds_read_codes16(a_cring + ((y_code + 16u * (unsigned)q) & (FL_CRING - 1)), Cl, Ch);
       };
       auto wait_flag = [&](unsigned addr, int& val, int need) __attribute__((always_inline)) {
         while (val < need) {
@@ -909,18 +954,20 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
 #if FL_HO == 2
       // every-lane hand-off: lanes 0..62 (and lane 63 with nothing to hand off) write to the
       // sink after the code copies (FL_SINK bytes, shared by the compute waves, never read)
-      const unsigned a_sink = lds_addr(codes + FL_NCOPY * L8) + 16u * (unsigned)lane;
-      const unsigned a_pa = (lane == 63) ? a_prog_me : lds_addr(codes + FL_NCOPY * L8) + 4u * (unsigned)lane;
+      const unsigned a_sink = lds_addr(codes + FL_NCOPY * FL_CSTR) + 16u * (unsigned)lane;
+      const unsigned a_pa = (lane == 63) ? a_prog_me : lds_addr(codes + FL_NCOPY * FL_CSTR) + 4u * (unsigned)lane;
 #endif
       unsigned plo, phi, plo2 = 0, phi2 = 0;
       fl_profile<GS, FLOOR>(kp.match, kp.mismatch, g, ac, plo, phi);
       if constexpr (R == 2) fl_profile<GS, FLOOR>(kp.match, kp.mismatch, g, ac2, plo2, phi2);
-      // LDS code address: column cs - lane + t, copy x = (cs - lane + OFF) & 7
-      unsigned a_code;
+      // LDS code address: column cs - lane + t, copy x = (cs - lane + OFF) & 7, ring byte
+      // (y_lane + 16 q) mod FL_CRING in phase q
+      unsigned a_cring, y_code;
       {
         const int c0 = cs - lane + FL_OFF;
         const int x = c0 & (FL_NCOPY - 1);
-        a_code = lds_addr(reinterpret_cast<int*>(codes + x * L8 + (c0 - x)));
+        a_cring = lds_addr(reinterpret_cast<int*>(codes + x * FL_CSTR));
+        y_code = (unsigned)(c0 - x);
       }
       // G-space: H = G - g(i+j), i+j = 64k + 1 + cs + t for every lane of step t
       const int negct0 = -g * (64 * k + 1 + cs);
@@ -952,7 +999,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         IN[1] = ds_read_b128<16>(ra);
         IN[2] = ds_read_b128<32>(ra);
         IN[3] = ds_read_b128<48>(ra);
-        CW = ds_read2_b64(a_code + 16 * q);
+        CW = ds_read2_b64(a_cring + ((y_code + 16u * (unsigned)q) & (FL_CRING - 1)));
       };
       auto reread_in = [&](int q, fl_v4i (&IN)[4]) __attribute__((always_inline)) {
         ds_reread_b128x4(a_ring_in + (unsigned)((q & (FL_RINGB - 1)) * 64), IN);

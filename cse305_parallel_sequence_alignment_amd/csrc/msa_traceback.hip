@@ -441,21 +441,23 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
   if (nops > cap && status == 0) status = -8;  // MSA_ERR_CAPACITY
   vm_wait_all();  // no load left in flight when the wave ends
   if (lane == 0) {
+    // info[0..3] (ops, begin, status) in every build: the callers check the status word
     info[0] = nops;
     info[1] = i + 1;
     info[2] = j + 1;
     info[3] = status;
+#ifdef MSA_TB_STATS
+    // diagnostic build (scripts/tb_stats.py): ticks prefetching, diagonal runs, windows, ticks inside
+    // groups (ticks waiting for group loads and the walk's total are derived there)
+    info[4] = t_pf;
+    info[5] = n_run;
+    info[6] = n_win;
+    info[7] = t_win;
+    (void)t_wait;
+#else
     info[4] = n_switch;
     info[5] = n_sync;
-#ifdef MSA_TB_STATS
-    info[2] = t_pf;
-    info[3] = n_run;
-    info[4] = t_wait;
-    info[5] = n_win;
-    info[7] = t_win;
-#endif
     info[6] = (long long)__builtin_amdgcn_s_memtime() - t_begin;  // s_memtime ticks, whole walk
-#ifndef MSA_TB_STATS
     info[7] = t_wait;
 #endif
   }

@@ -144,7 +144,9 @@ def optimal_alignment_distributed(A1: bytes, B1: bytes, m: int, n: int, p: int, 
         except Exception as e:  # the other ranks must not wait on the broadcast forever
             box[0] = RuntimeError(f"rank 0: partition failed: {e}")
     if world > 1 and bp is None:
-        dist.broadcast_object_list(box, src=0, group=group)
+        # src is a GLOBAL rank: the group's rank 0 (which computed the partition above)
+        src = dist.get_global_rank(group, 0) if group is not None else 0
+        dist.broadcast_object_list(box, src=src, group=group)
     if isinstance(box[0], Exception):
         raise box[0]
     points = [tuple(int(v) for v in x) for x in box[0]]
@@ -163,11 +165,21 @@ def optimal_alignment_distributed(A1: bytes, B1: bytes, m: int, n: int, p: int, 
             torch.cuda.set_device(dev)
         return solve(A1, B1, points, k, g, h)
 
-    with ThreadPoolExecutor(max_workers=max(1, min(8, len(mine)))) as pool:
-        local = dict(zip(mine, pool.map(run, mine)))
+    # a failing subproblem must not leave this rank out of the all-gather (the others would wait in it
+    # until the backend's timeout): the error travels in the gathered dict and every rank raises it
+    try:
+        with ThreadPoolExecutor(max_workers=max(1, min(8, len(mine)))) as pool:
+            local = dict(zip(mine, pool.map(run, mine)))
+    except Exception as e:
+        if world == 1:
+            raise
+        local = {"__err__": f"rank {rank}: subproblem failed: {e!r}"}
     if world > 1:
         every: List[Optional[Dict[int, List[Node]]]] = [None] * world
         dist.all_gather_object(every, local, group=group)
+        errs = [d["__err__"] for d in every if "__err__" in d]
+        if errs:
+            raise RuntimeError("; ".join(errs))
         solved: Dict[int, List[Node]] = {}
         for d in every:
             solved.update(d)

@@ -21,6 +21,9 @@
  *   orc_print_seq          main_alignment.cpp:32-55
  *   orc_main_alignment     main_alignment.cpp:11-22 (OptimalAlignmentMapThread),
  *                          :202-351 (single-subproblem path), :353-410
+ *   orc_main_alignment_dir the same path for integral g, h in 1 B/cell (direction
+ *                          bytes + int64 rows) for the callers' whole-sequence sizes
+ *                          (testing.cpp:261,345); equals orc_main_alignment
  *   orc_optimal_alignment  main_alignment.cpp:202-351 (subproblem selection of the
  *                          three rounds :232-341, stitch :344-348 incl. the
  *                          never-made link into the last subproblem), :32-55
@@ -238,6 +241,115 @@ int64_t orc_main_alignment(const char* A, const char* B, uint64_t m, uint64_t n,
   memcpy(out + o, l2, len); o += len; out[o++] = '\n';
   out[o] = 0;
   free(l1); free(l2); free(nodes);
+  return (int64_t)o;
+}
+
+/* orc_main_alignment at the reference callers' sizes (testing.cpp:261,345 pass whole
+ * sequences, 13k-97k): the same single-subproblem path with integral g, h, in O(m n)
+ * BYTES instead of three (m+1)(n+1) double tables.  Rows of T1/T2/T3 are int64 (the
+ * reference's doubles hold exact integers here; -inf is a sentinel far below every
+ * finite value, and every interior cell of start type -1 is finite, so no sum ever
+ * involves it except as a losing candidate).  Each cell keeps one byte: bits 0-1 the
+ * table find_alignment's T1 branch picks (the first of T1, T2, T3 at (i-1,j-1) whose
+ * value equals the cell minus f, :150-155), bits 2-3 its T2 branch (:157-163), bits
+ * 4-5 its T3 branch (:164-171) -- the first table in the reference's order that
+ * reproduces the cell, i.e. the first maximum of the recurrence's candidates
+ * (:396-398).  The walk then follows find_alignment (:105-172, quirks Q1/Q2, end rule
+ * with end_type -1) and print_seq (main_alignment.cpp:32-55) over the unswapped
+ * arrays.  Same output contract as orc_main_alignment. */
+int64_t orc_main_alignment_dir(const char* A, const char* B, uint64_t m, uint64_t n, int64_t g, int64_t h,
+                               char* out, uint64_t cap, int64_t* score) {
+  const int swap = m > n;
+  const char* sA = swap ? B : A;
+  const char* sB = swap ? A : B;
+  const uint64_t mm = swap ? n : m, nn = swap ? m : n, W = nn + 1;
+  const int64_t NI = -((int64_t)1 << 50), GH = g + h;
+  uint8_t* dir = (uint8_t*)malloc((mm + 1) * W);
+  int64_t* rows = (int64_t*)malloc(sizeof(int64_t) * 6 * W);
+  orc_node* nodes = (orc_node*)malloc(sizeof(orc_node) * (m + n + 2));
+  if (!dir || !rows || !nodes) { free(dir); free(rows); free(nodes); return ORC_ERR_NOMEM; }
+  int64_t *p1 = rows, *p2 = rows + W, *p3 = rows + 2 * W, *c1 = rows + 3 * W, *c2 = rows + 4 * W, *c3 = rows + 5 * W;
+  /* row 0, start type -1 (compute_row(0), subproblem_alignment.cpp:212-227, :259-280) */
+  p1[0] = 0; p2[0] = NI; p3[0] = NI;
+  for (uint64_t j = 1; j <= nn; j++) { p1[j] = NI; p3[j] = NI; p2[j] = -h - g * (int64_t)j; }
+  for (uint64_t i = 1; i <= mm; i++) {
+    c1[0] = NI; c2[0] = NI; c3[0] = -h - g * (int64_t)i; /* :282-292 */
+    const char a = sA[i];
+    uint8_t* drow = dir + i * W;
+    for (uint64_t j = 1; j <= nn; j++) {
+      const int64_t f = (a == sB[j]) ? 1 : 0;
+      /* T1: f + max(T1, T2, T3)(i-1, j-1); first maximum in table order */
+      int64_t v1 = p1[j - 1]; unsigned k1 = 1;
+      if (p2[j - 1] > v1) { v1 = p2[j - 1]; k1 = 2; }
+      if (p3[j - 1] > v1) { v1 = p3[j - 1]; k1 = 3; }
+      /* T2: max(T1 - g - h, T2 - g, T3 - g - h)(i, j-1) */
+      int64_t v2 = c1[j - 1] - GH; unsigned k2 = 1;
+      if (c2[j - 1] - g > v2) { v2 = c2[j - 1] - g; k2 = 2; }
+      if (c3[j - 1] - GH > v2) { v2 = c3[j - 1] - GH; k2 = 3; }
+      /* T3: max(T1 - g - h, T2 - g - h, T3 - g)(i-1, j) */
+      int64_t v3 = p1[j] - GH; unsigned k3 = 1;
+      if (p2[j] - GH > v3) { v3 = p2[j] - GH; k3 = 2; }
+      if (p3[j] - g > v3) { v3 = p3[j] - g; k3 = 3; }
+      c1[j] = f + v1;
+      c2[j] = v2;
+      c3[j] = v3;
+      drow[j] = (uint8_t)(k1 | (k2 << 2) | (k3 << 4));
+    }
+    int64_t* t;
+    t = p1; p1 = c1; c1 = t;
+    t = p2; p2 = c2; c2 = t;
+    t = p3; p3 = c3; c3 = t;
+  }
+  /* final cell (p* hold row mm): find_alignment's end rule with end_type -1 (:112-146) */
+  const int64_t t1 = p1[nn], t2 = p2[nn], t3 = p3[nn];
+  if (score) *score = t1 > t2 ? (t1 > t3 ? t1 : t3) : (t2 > t3 ? t2 : t3);
+  free(rows);
+  orc_node* tmp = (orc_node*)malloc(sizeof(orc_node) * (mm + nn + 2));
+  if (!tmp) { free(dir); free(nodes); return ORC_ERR_NOMEM; }
+  uint64_t i = mm, j = nn, cnt = 0;
+  orc_node cur;
+  cur.pad = 0;
+  if (t1 >= t2 && t1 >= t3) { cur.t = 1; cur.i = i; cur.j = j; }
+  else if (t2 >= t1 && t2 >= t3) { cur.t = 2; cur.i = 0; cur.j = j; }
+  else { cur.t = 3; cur.i = i; cur.j = 0; }
+  tmp[cnt++] = cur;
+  int ct = cur.t;
+  while (i > 0 && j > 0) {
+    const unsigned d = dir[i * W + j];
+    orc_node nw;
+    nw.pad = 0;
+    const int nt = (int)((d >> (2 * (ct - 1))) & 3u);
+    nw.t = nt;
+    if (ct == 1) { /* :150-156 (Q2: the T1 -> T1 node's j uses idA, 0 here) */
+      nw.i = (nt == 2) ? 0 : i - 1;
+      nw.j = (nt == 3) ? 0 : j - 1;
+      i--; j--;
+    } else if (ct == 2) { /* :157-163 */
+      nw.i = (nt == 2) ? 0 : i;
+      nw.j = (nt == 3) ? 0 : j - 1;
+      j--;
+    } else { /* :164-171 */
+      nw.i = (nt == 2) ? 0 : i - 1;
+      nw.j = (nt == 3) ? 0 : j;
+      i--;
+    }
+    ct = nt;
+    tmp[cnt++] = nw;
+  }
+  free(dir);
+  const uint64_t len = cnt - 1; /* Q1: the last-created node is dropped (:170) */
+  for (uint64_t k = 0; k < len; k++) nodes[k] = tmp[cnt - 2 - k];
+  free(tmp);
+  const char* hdr = "bp1\nbp1.2\nbp2\nbp3\nbp4\n";
+  const uint64_t need = strlen(hdr) + 2 * (len + 1) + 1;
+  if (need > cap) { free(nodes); return ORC_ERR_CAP; }
+  uint64_t o = 0;
+  memcpy(out + o, hdr, strlen(hdr)); o += strlen(hdr);
+  orc_print_seq(A, B, m, n, nodes, len, out + o, out + o + len + 1); /* unswapped arrays (Q3) */
+  o += len; out[o++] = '\n';
+  o += len; out[o++] = '\n';
+  out[o] = 0;
+  free(nodes);
   return (int64_t)o;
 }
 

@@ -54,6 +54,8 @@ def lib():
                                                P, u64, P, P]
         L.orc_main_alignment.argtypes = [P, P, u64, u64, C.c_double, C.c_double, P, u64, P]
         L.orc_main_alignment.restype = C.c_int64
+        L.orc_main_alignment_dir.argtypes = [P, P, u64, u64, C.c_int64, C.c_int64, P, u64, P]
+        L.orc_main_alignment_dir.restype = C.c_int64
         L.orc_optimal_alignment.argtypes = [P, P, u64, u64, P, u64, C.c_double, C.c_double, C.c_int, P, u64, P,
                                             u64, P]
         L.orc_optimal_alignment.restype = C.c_int64
@@ -135,6 +137,20 @@ def main_alignment_text(A: bytes, B: bytes, g=1.0, h=2.0):
     if rc < 0:
         raise RuntimeError(f"oracle main_alignment rc={rc}")
     return out[:rc].tobytes().decode("latin-1"), score.value
+
+
+def main_alignment_text_dir(A: bytes, B: bytes, g=1, h=2):
+    """main_alignment_text for integral g, h in 1 B/cell (orc_main_alignment_dir): the reference
+    callers' whole-sequence sizes (13k-97k) without three (m+1)(n+1) double tables."""
+    a, b = _bytes1(A), _bytes1(B)
+    cap = 64 + 2 * (len(A) + len(B) + 4)
+    out = np.zeros(cap, dtype=np.uint8)
+    score = C.c_int64(0)
+    rc = lib().orc_main_alignment_dir(_ptr(a), _ptr(b), len(A), len(B), int(g), int(h), _ptr(out), cap,
+                                      C.byref(score))
+    if rc < 0:
+        raise RuntimeError(f"oracle main_alignment_dir rc={rc}")
+    return out[:rc].tobytes().decode("latin-1"), float(score.value)
 
 
 def optimal_alignment(A: bytes, B: bytes, bp, g=1.0, h=2.0, fix_all=False):

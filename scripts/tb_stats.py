@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Diagnostic (needs a -DMSA_TB_STATS build of libmsa.so): where the device walk's time goes, for
 the C5 (SW affine) and ref (Gotoh, 10k) walks.  In that build the walk's info words are
-{ops, -, ticks prefetching, diagonal runs, ticks waiting for group loads, windows, ticks total,
-ticks inside groups}.
+{ops, begin i, begin j, status, ticks prefetching, diagonal runs, windows, ticks inside groups};
+the walk's total comes from HIP events around it.
 
     python3 scripts/tb_stats.py --workload c5
 """
@@ -34,15 +34,19 @@ out = torch.empty(pl.cells_elems, dtype=torch.uint8, device="cuda")
 ops = torch.empty(len(A) + len(B) + 16, dtype=torch.uint8, device="cuda")
 info = torch.zeros(8, dtype=torch.int64, device="cuda")
 pl.run(dA, dB, out)
-rows = []
+rows, ms = [], []
 for rep in range(4):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
     if args.workload == "c5":
         pl.traceback_async(out, ops, info)
     else:
         pl.traceback_gotoh_async(out, ops, info, -1)
+    e1.record()
     torch.cuda.synchronize()
     rows.append(info.cpu().tolist())
+    ms.append(e0.elapsed_time(e1))
 k = rows[-1]
-print(json.dumps(dict(workload=args.workload, ops=k[0], t_prefetch=k[2], n_run=k[3], t_wait=k[4], n_win=k[5],
-                      t_total=k[6], t_in_groups=k[7], t_other=k[6] - k[7] - k[2] - k[4],
-                      totals=[r[6] for r in rows])), flush=True)
+assert k[3] == 0, f"walk status {k[3]}"
+print(json.dumps(dict(workload=args.workload, ops=k[0], t_prefetch=k[4], n_run=k[5], n_win=k[6], t_in_groups=k[7],
+                      walk_ms=[round(x, 4) for x in ms])), flush=True)

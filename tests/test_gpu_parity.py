@@ -116,8 +116,9 @@ def test_sw_linear_single_score_only(oracle, dev, LB, scoring, track_end):
 
 
 @pytest.mark.parametrize("track_end", [False, True])
-def test_sw_linear_single_wide_pair_stripe_kernel(oracle, dev, LB, track_end):
-    """Pairs too wide for the flow kernel's LDS code copies (n > ~19.5k) run the one-pass stripe kernel."""
+def test_sw_linear_single_wide_pair_flow_kernel(oracle, dev, LB, track_end):
+    """Pairs wider than the former whole-row LDS code copies (n > ~19.5k) run the two-pass flow kernel too (the
+    column codes stream through LDS rings): R = 2 layout, H and the first-maximum end equal the oracle's."""
     import torch
     from cse305_parallel_sequence_alignment_amd.plan import Plan
 
@@ -126,7 +127,7 @@ def test_sw_linear_single_wide_pair_stripe_kernel(oracle, dev, LB, track_end):
         A, B = rs(rng, m), rs(rng, n)
         pl = Plan(LB.SW_LINEAR, LB.CELLS_H, [m], [n], [0], [0], match=ma, mismatch=mi, gap_open=g, gap_extend=g,
                   track_end=track_end, single=True)
-        assert pl.geom[0].rows_per_lane == 1
+        assert pl.geom[0].rows_per_lane == 2
         H = torch.empty(pl.cells_elems, dtype=torch.int32, device=dev)
         pl.run(_dev(A, dev), _dev(B, dev), H)
         res = pl.results()[0]
@@ -809,6 +810,91 @@ def test_gotoh_flow_dir_bytes(dev, LB, gh, m, n):
     assert mode1 == "flow"
     assert (s1, f1) == (s0, f0)
     assert np.array_equal(d1[1:, 1:] & 63, d0[1:, 1:] & 63)
+
+
+def _gotoh_tags(T1, T2, T3, g, h):
+    """The REF1 tag byte of every cell from the reference's double tables: bits 0-1 / 2-3 / 4-5 = 4 - the table
+    find_alignment's T1 / T2 / T3 branch picks (the first of T1, T2, T3 whose candidate is the maximum,
+    subproblem_alignment.cpp:150-171)."""
+    def first(c):
+        return 4 - np.argmax(np.stack(c), axis=0).astype(np.uint8) - 1
+
+    t1 = first([T1[:-1, :-1], T2[:-1, :-1], T3[:-1, :-1]])
+    t2 = first([T1[1:, :-1] - g - h, T2[1:, :-1] - g, T3[1:, :-1] - g - h])
+    t3 = first([T1[:-1, 1:] - g - h, T2[:-1, 1:] - g - h, T3[:-1, 1:] - g])
+    return t1 | (t2 << 2) | (t3 << 4)
+
+
+@pytest.mark.parametrize("m,n", [(130, 45000), (300, 61000), (1000, 20100), (64, 9000)])
+def test_flow_kernels_wide_pairs(oracle, dev, LB, m, n):
+    """Column codes stream through fixed LDS rings in the flow kernels: pairs far wider than the former
+    whole-row LDS copies (SW linear n <= ~19.5k, affine / Gotoh n <= ~37k) run the flow kernels (run_info mode
+    1); the ring wraps every 4 KiB of columns.  Gotoh: the tag byte of every cell equals the one derived from
+    the oracle's tables, and the device walk equals the oracle's node list; affine SW: score, end, begin and
+    CIGAR of the device traceback equal the oracle's; SW linear: the checksum of the whole H matrix."""
+    import torch
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+
+    rng = np.random.default_rng(m + n)
+    A, B = _mutated(rng, m, n)
+    dA, dB = _dev(A, dev), _dev(B, dev)
+    pl = Plan(LB.REF_GOTOH, LB.CELLS_DIR, [m], [n], [0], [0], match=1, mismatch=0, gap_open=3, gap_extend=1,
+              start_type=-1)
+    D = torch.empty(pl.cells_elems, dtype=torch.uint8, device=dev)
+    pl.run(dA, dB, D)
+    assert pl.run_info()["mode"] == "flow"
+    r = pl.results()[0]
+    tb = pl.traceback_gotoh(D, end_type=-1)
+    o = oracle.subproblem_align(A, B, -1, -1, 1.0, 2.0)
+    fin = tuple(float(T[m, n]) for T in (o["T1"], o["T2"], o["T3"]))
+    assert tuple(float(x) for x in r["fin"]) == fin
+    ts = [t for (_, _, t) in o["nodes"]]
+    assert tb["ops"].decode() == "".join("MDI"[t - 1] for t in reversed(ts))
+    d = pl.deskew_dir(D.cpu().numpy(), 0, pl.stripe_meta())
+    assert np.array_equal(d[1:, 1:] & 63, _gotoh_tags(o["T1"], o["T2"], o["T3"], 1.0, 2.0))
+    del o, d
+    pl = Plan(LB.SW_AFFINE, LB.CELLS_DIR, [m], [n], [0], [0], match=2, mismatch=-3, gap_open=5, gap_extend=2,
+              track_end=True)
+    D = torch.empty(pl.cells_elems, dtype=torch.uint8, device=dev)
+    pl.run(dA, dB, D)
+    assert pl.run_info()["mode"] == "flow"
+    tb = pl.traceback(D)
+    o = oracle.sw(A, B, 2, -3, 5, 2, want_tb=True)
+    r = pl.results()[0]
+    assert (r["score"], tuple(r["end"]), tuple(tb["beg"]), tb["cigar"]) == \
+        (o["score"], tuple(o["end"]), tuple(o["beg"]), o["cigar"])
+    assert pl.error() == 0
+    pl = Plan(LB.SW_LINEAR, LB.CELLS_H, [m], [n], [0], [0], match=1, mismatch=0, gap_open=1, gap_extend=1)
+    H = torch.empty(pl.cells_elems, dtype=torch.int32, device=dev)
+    pl.run(dA, dB, H)
+    o = oracle.sw(A, B, 1, 0, 1, 1, want_h=True)
+    assert pl.run_info()["mode"] == "flow"
+    assert pl.results()[0]["score"] == o["score"]
+    assert pl.checksum(H) == oracle.checksum_h(o["H"])
+
+
+@pytest.mark.parametrize("how", ["batch_of_one", "g16_single"])
+def test_ref1_stripe_layout_walk(oracle, dev, LB, how):
+    """The tagged REF1 fill in the one-pass stripe kernel (a one-pair batch, or a single pair whose profile bytes
+    4 (f + 2g) do not fit int8, g = 16) and find_alignment's device walk over the STRIPE layout (stripe starts
+    read from the meta, csflow = 0): the ops equal the oracle's node list."""
+    import torch
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+
+    g, h = (1, 2) if how == "batch_of_one" else (16, 3)
+    rng = np.random.default_rng(77 + g)
+    for (m, n) in [(1, 1), (5, 300), (65, 66), (700, 701), (1000, 1300), (2600, 900), (3000, 3100)]:
+        A, B = _mutated(rng, m, n) if m > 100 else (rs(rng, m), rs(rng, n))
+        pl = Plan(LB.REF_GOTOH, LB.CELLS_DIR, [m], [n], [0], [0], match=1, mismatch=0, gap_open=g + h,
+                  gap_extend=g, start_type=-1, single=(how != "batch_of_one"))
+        D = torch.empty(pl.cells_elems, dtype=torch.uint8, device=dev)
+        pl.run(_dev(A, dev), _dev(B, dev), D)
+        assert pl.run_info()["mode"] == "stripe"
+        tb = pl.traceback_gotoh(D, end_type=-1)
+        o = oracle.subproblem_align(A, B, -1, -1, float(g), float(h))
+        ts = [t for (_, _, t) in o["nodes"]]
+        want = "".join("MDI"[t - 1] for t in reversed(ts)) if ts else "MDI"[o["end"][2] - 1]
+        assert tb["ops"].decode() == want, (m, n, how)
 
 
 @pytest.mark.parametrize("gap", [("B", 300), ("A", 300), ("B", 700), ("A", 70), ("both", 260)])

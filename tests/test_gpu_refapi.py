@@ -118,6 +118,55 @@ def test_concurrent_main_alignment(oracle, dev, dataset):
         assert g == w, (len(A), len(B))
 
 
+WHOLE = json.loads((GOLDEN / "whole.json").read_text())
+
+
+@pytest.mark.parametrize("c", WHOLE, ids=[f"{c['a']}x{c['b']}_{c['m']}x{c['n']}" for c in WHOLE])
+def test_main_alignment_whole_sequences(oracle, dev, dataset, c):
+    """main_alignment_function at the sizes its own callers use: testing.cpp:261 / :345 align WHOLE sequences of
+    the bundled file (13,309-97,409 characters).  The text (bp lines, both print_seq lines) equals the 1 B/cell
+    oracle's (tests/golden/whole.json, make_whole.py; the oracle reproduces the reference's own 10k / 20k
+    outputs) -- whole TP53 (also against the oracle live), 48k x 47k (m > n, > 2^31 direction bytes), a
+    dissimilar 40k pair, whole ABCB1 x ABCB1 (97,409 x 97,403: 9.5 GB of direction bytes) and whole CDH1."""
+    import hashlib
+
+    from cse305_parallel_sequence_alignment_amd import api
+
+    _, seqs = dataset
+    A = seqs[c["a"]] if c["La"] is None else seqs[c["a"]][:c["La"]]
+    B = seqs[c["b"]] if c["Lb"] is None else seqs[c["b"]][:c["Lb"]]
+    text, score = api.main_alignment_text(b"\0" + A, b"\0" + B, len(A), len(B), 64, 1, 2)
+    lines = text.split("\n")[5:7]
+    assert score == c["score"] and len(lines[0]) == c["n_nodes"]
+    assert hashlib.md5((lines[0] + "\n" + lines[1] + "\n").encode()).hexdigest() == c["lines_md5"]
+    assert hashlib.md5(text.encode("latin-1")).hexdigest() == c["text_md5"]
+    if len(A) * len(B) < 3e8:
+        assert text == oracle.main_alignment_text_dir(A, B, 1, 2)[0]
+
+
+def test_concurrent_main_alignment_at_size(dev, dataset):
+    """8 host threads call msa_main_alignment at 10k-20k at once: several two-pass flow launches share the GPU
+    (pass-1 roles by arrival ticket, the first item of every XCD chunk claimed by an early arrival); every
+    text equals the reference's own output (at_size.json)."""
+    import hashlib
+
+    from cse305_parallel_sequence_alignment_amd import api
+
+    _, seqs = dataset
+    cases = [c for c in json.loads((GOLDEN / "at_size.json").read_text())] * 4
+
+    def one(c):
+        A, B = seqs[c["a"]][:c["L"]], seqs[c["b"]][:c["L"]]
+        t, sc = api.main_alignment_text(b"\0" + A, b"\0" + B, c["L"], c["L"], 32, c["g"], c["h"])
+        lines = t.split("\n")[5:7]
+        return sc, hashlib.md5((lines[0] + "\n" + lines[1] + "\n").encode()).hexdigest()
+
+    with ThreadPoolExecutor(max_workers=8) as ex:
+        got = list(ex.map(one, cases))
+    for (sc, md5), c in zip(got, cases):
+        assert (sc, md5) == (c["score"], c["lines_md5"]), c
+
+
 # ---- the reference's class Subproblem through libmsa_compat.so (C++ drop-in) ----
 
 ROOT = GOLDEN.parent.parent

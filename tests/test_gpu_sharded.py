@@ -1,0 +1,93 @@
+"""The C4 sharding path with its DEVICE scorer at world size 2 (both ranks on the box's one GPU, gloo
+carrying the broadcast and the all-gather of device tensors): every rank fills its block of the 1024
+4,000 x 4,000 pairs with a Plan (libmsa.so), copies the scores device-to-device, and the gathered
+vector equals the committed fixture (tests/golden/c4_scores.json, made by the oracle).  bench.py's c4
+workload runs exactly this code with RCCL over xGMI, one GPU per rank; tests/test_dist_gloo.py runs it
+with the oracle as scorer on CPU."""
+import json
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    import sys
+    import traceback
+
+    from conftest import ROOT
+
+    sys.path.insert(0, str(ROOT))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        import torch
+        import torch.distributed as dist
+
+        from cse305_parallel_sequence_alignment_amd import _lib as LB
+        from cse305_parallel_sequence_alignment_amd import data
+        from cse305_parallel_sequence_alignment_amd.plan import Plan
+        from cse305_parallel_sequence_alignment_amd.shard import ShardedBatch, broadcast_reference, shard_range
+
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        try:
+            dev = torch.device("cuda", 0)
+            total, L = data.C4_PAIRS, data.C4_LEN
+            lo, hi = shard_range(total, rank, world)
+            qs = data.c4_queries(lo, hi)
+            # only rank 0 holds the reference sequence; the broadcast gives it to every rank
+            ref = torch.from_numpy(data.encode(data.c4_reference())).to(dev) if rank == 0 else \
+                torch.zeros(L, dtype=torch.uint8, device=dev)
+            dB = broadcast_reference(ref)
+            dA = torch.from_numpy(data.encode(b"".join(qs))).to(dev)
+            plan = Plan(LB.SW_LINEAR, LB.CELLS_NONE, [L] * len(qs), [L] * len(qs), [k * L for k in range(len(qs))],
+                        [0] * len(qs), match=1, mismatch=0, gap_open=1, gap_extend=1)
+            local = torch.empty(len(qs), dtype=torch.int32, device=dev)
+
+            def score_block(lo_, hi_):
+                assert (lo_, hi_) == (lo, hi)
+                plan.run(dA, dB)
+                plan.scores_into(local)
+                return local
+
+            batch = ShardedBatch(total, rank, world, score_block)
+            got = [batch.step().cpu().tolist() for _ in range(2)]
+            q.put((rank, dict(scores=got, err=plan.error(), n=hi - lo)))
+        finally:
+            dist.destroy_process_group()
+    except Exception:
+        q.put((rank, traceback.format_exc()))
+
+
+def test_c4_sharded_device_world2(dev):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    try:
+        out = dict(q.get(timeout=100) for _ in ps)
+    finally:
+        for p in ps:
+            p.join(timeout=20)
+            if p.is_alive():
+                p.kill()
+    want = json.loads((GOLDEN / "c4_scores.json").read_text())["scores"]
+    for r in range(world):
+        assert not isinstance(out[r], str), out[r]
+        assert out[r]["err"] == 0
+        assert out[r]["n"] == 512
+        for step in out[r]["scores"]:
+            assert step == want

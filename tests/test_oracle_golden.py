@@ -127,6 +127,42 @@ def test_oracle_at_size_10k(oracle, dataset):
         assert hashlib.md5((lines[0] + "\n" + lines[1] + "\n").encode()).hexdigest() == c["lines_md5"]
 
 
+def test_oracle_dir_at_size(oracle, dataset):
+    """orc_main_alignment_dir (1 B/cell, for the callers' whole-sequence sizes) reproduces the reference's own
+    10k and 20k outputs (at_size.json: score, node count, md5 of the print_seq lines)."""
+    _, seqs = dataset
+    for c in json.loads((GOLDEN / "at_size.json").read_text()):
+        A, B = seqs[c["a"]][:c["L"]], seqs[c["b"]][:c["L"]]
+        text, score = oracle.main_alignment_text_dir(A, B, int(c["g"]), int(c["h"]))
+        lines = text.split("\n")[5:7]
+        assert score == c["score"] and len(lines[0]) == c["n_nodes"], c
+        assert hashlib.md5((lines[0] + "\n" + lines[1] + "\n").encode()).hexdigest() == c["lines_md5"], c
+
+
+def test_oracle_dir_equals_double_tables(oracle, dataset):
+    """orc_main_alignment_dir == orc_main_alignment (the reference's double tables restated) byte for byte:
+    random and mutated pairs, m < n and m > n (the ctor's swap, print_seq over the unswapped arrays), several
+    (g, h), the KATs and the harness pairs."""
+    rng = np.random.default_rng(404)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    cases = [(b"AGGA", b"AGTGC", 1, 2), (b"AGGA", b"ATGTC", 2, 1)]
+    for _ in range(40):
+        m, n = (int(x) for x in rng.integers(1, 160, size=2))
+        A = rng.choice(acgt, m).tobytes()
+        B = bytearray(A[:n] + rng.choice(acgt, max(0, n - m)).tobytes())
+        for k in rng.choice(len(B), size=len(B) // 6 + 1, replace=False):
+            B[k] = int(rng.choice(acgt))
+        g, h = [(1, 2), (2, 1), (1, 0), (3, 5)][int(rng.integers(4))]
+        cases.append((A, bytes(B), g, h))
+    _, seqs = dataset
+    for hp in KAT["harness"]:
+        cases.append((seqs[hp["a"]][:hp["L"]], seqs[hp["b"]][:hp["L"]], 1, 2))
+    cases.append((seqs[3][:1800], seqs[7][:1500], 1, 2))
+    for A, B, g, h in cases:
+        assert oracle.main_alignment_text_dir(A, B, g, h) == oracle.main_alignment_text(A, B, float(g), float(h)), \
+            (len(A), len(B), g, h)
+
+
 def test_at_size_scores_are_the_surveyed_ones():
     """at_size.json holds the reference scores SURVEY.md §8(c) probed: 8094 / 8112 (h=0) / 18049 / 6522."""
     got = {(c["a"], c["b"], c["L"], c["h"]): c["score"] for c in json.loads((GOLDEN / "at_size.json").read_text())}

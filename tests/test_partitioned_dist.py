@@ -177,6 +177,82 @@ def test_partitioned_world(world):
     _check(out, world)
 
 
+def _worker_edge(rank, world, port, q):
+    """A subgroup whose rank 0 is not global rank 0 (ranks [1, 2] of world 3), and a subproblem that fails
+    on one rank (world-wide: every rank raises instead of waiting in the all-gather)."""
+    import sys
+    import traceback
+
+    from conftest import ROOT
+
+    sys.path.insert(0, str(ROOT))
+    import torch.distributed as dist
+
+    from cse305_parallel_sequence_alignment_amd.partitioned import optimal_alignment_distributed
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        try:
+            part, solve = _oracle_fns()
+            A, B = _pair(300, 280, 3)
+            sub = dist.new_group([1, 2])
+            out = {}
+            if rank in (1, 2):
+                def part1(*a):
+                    assert rank == 1, "only the group's rank 0 (global rank 1) finds the partition"
+                    return part(*a)
+
+                out["sub"] = optimal_alignment_distributed(b"\0" + A + b"\0", b"\0" + B + b"\0", 300, 280, 8, 1.0,
+                                                           2.0, fix_all=True, partition_fn=part1, solve_fn=solve,
+                                                           group=sub)[0]
+
+            def bad(A1, B1, bp, k, g, h):
+                if rank == world - 1:
+                    raise RuntimeError("injected solve failure")
+                return solve(A1, B1, bp, k, g, h)
+
+            try:
+                optimal_alignment_distributed(b"\0" + A + b"\0", b"\0" + B + b"\0", 300, 280, 8, 1.0, 2.0,
+                                              fix_all=True, partition_fn=part, solve_fn=bad)
+                out["fail"] = "no error"
+            except RuntimeError as e:
+                out["fail"] = str(e)
+            q.put((rank, out))
+        finally:
+            dist.destroy_process_group()
+    except Exception:
+        q.put((rank, traceback.format_exc()))
+
+
+def test_partitioned_subgroup_and_solve_failure():
+    from oracle import oracle as O
+
+    O.build()
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_edge, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    try:
+        out = dict(q.get(timeout=120) for _ in ps)
+    finally:
+        for p in ps:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        assert not isinstance(out[r], str), out[r]
+    A, B = _pair(300, 280, 3)
+    bp = O.partial_partition(A, B, 8, 1.0, 2.0, -1, -1)
+    want, _ = O.optimal_alignment(A, B, bp, 1.0, 2.0, True)
+    assert out[1]["sub"] == out[2]["sub"] == want
+    for r in range(world):
+        assert "injected solve failure" in out[r]["fail"] and f"rank {world - 1}" in out[r]["fail"], out[r]
+
+
 def test_partitioned_world1_matches_oracle():
     """No process group: the same code on one rank (the GPU box's world-1 run)."""
     from oracle import oracle as O
