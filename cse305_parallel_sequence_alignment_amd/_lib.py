@@ -13,7 +13,8 @@ import os
 from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
-LIB_PATH = PKG / "libmsa.so"
+# MSA_LIB_PATH: a diagnostic build (e.g. -DMSA_STAMPS) loaded instead of the in-tree library
+LIB_PATH = Path(os.environ.get("MSA_LIB_PATH", str(PKG / "libmsa.so")))
 
 MSA_OK = 0
 STATUS = {

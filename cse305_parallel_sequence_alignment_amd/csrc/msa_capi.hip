@@ -241,15 +241,23 @@ int device_cus() {
   cus[dev] = n;
   return n;
 }
-// sets the kernel's dynamic-LDS limit and returns its occupancy (blocks per CU, >= 1), or -1
+// raises the kernel's dynamic-LDS limit to the CU's whole LDS (once per device and kernel: plans of
+// one kernel with different LDS sizes then never lower it under each other) and returns its
+// occupancy at `lds` bytes (blocks per CU, >= 1), or -1
 int kernel_shape(kfn_t fn, int threads, size_t lds) {
   static std::map<std::tuple<int, kfn_t, int, size_t>, int> occ_of;
+  static std::map<std::pair<int, kfn_t>, bool> attr_set;
   const auto key = std::make_tuple(current_device(), fn, threads, lds);
   std::lock_guard<std::mutex> lk(g_shape_mu);
   auto it = occ_of.find(key);
   if (it != occ_of.end()) return it->second;
-  if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-    return -1;
+  if (lds > 160 * 1024) return -1;
+  const auto ak = std::make_pair(current_device(), fn);
+  if (!attr_set[ak]) {
+    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+      return -1;
+    attr_set[ak] = true;
+  }
   int occ = 1;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)fn, threads, lds) != hipSuccess || occ < 1)
     occ = 1;
@@ -527,18 +535,8 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   // reference-Gotoh (start type -1, tagged) pair with direction bytes (two values per link
   // column, 4 code rings); the column codes stream through fixed-size LDS rings, so any n fits
   const bool aff = kalg == MSA_ALG_SWA || kalg == MSA_ALG_REF1;
-  size_t flow_lds = (size_t)(FL_FLAGS + (FL_W + 1) * 256 * (aff ? 2 : 1)) * 4 +
-                    (size_t)(aff ? 4 : FL_NCOPY) * FL_CSTR + ((aff || FL_HO != 2) ? 0 : FL_SINK);
-  // One flow workgroup per CU: a pass-2 workgroup sharing a CU with a pass-1 one would take issue
-  // slots from its chain waves (one chain wave keeps its SIMD's issue busy most of each step,
-  // DESIGN §5).  MSA_FLOW_LDS_MIN (bytes, diagnostic) overrides the floor.
-  {
-    static const long lds_min = [] {
-      const char* e = std::getenv("MSA_FLOW_LDS_MIN");
-      return e ? std::strtol(e, nullptr, 10) : 80 * 1024 + 1024;
-    }();
-    flow_lds = std::max(flow_lds, (size_t)std::max(0L, lds_min));
-  }
+  const size_t flow_lds = (size_t)(FL_FLAGS + (FL_W + 1) * 256 * (aff ? 2 : 1)) * 4 +
+                          (size_t)(aff ? 4 : FL_NCOPY) * FL_CSTR + ((aff || FL_HO != 2) ? 0 : FL_SINK);
   // affine: profile bytes score + 2e + (o - e) must be int8
   const bool aff_ok = kalg == MSA_ALG_SWA && out_mode == MSA_OUT_DIR && desc->gap_extend >= 0 &&
                       desc->gap_open >= desc->gap_extend &&
@@ -696,8 +694,8 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   if (flow) {
     kp.lds_code_bytes = fl_code_bytes((int)desc->n[0]);
     P->lds_bytes = flow_lds;
-    // pass-2 blocks: 544 ints per wave past the flags
-    if (P->flow2) P->lds_bytes = std::max(flow_lds, (size_t)(FL_FLAGS + (FL_W + 2) * 544) * 4);
+    // pass-2 blocks: FL_P2INTS ints per wave (inputs + column codes staged in LDS)
+    if (P->flow2) P->lds_bytes = std::max(flow_lds, (size_t)(FL_W + 2) * FL_P2INTS * 4);
   }
   if (P->lds_bytes > 160 * 1024) {
     std::fprintf(stderr, "msa: problem needs %zu B of LDS per workgroup (> 160 KiB)\n", P->lds_bytes);
@@ -713,17 +711,47 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   const int cap = ncu * std::min(occ, 2);
   P->grid = std::max(1, std::min(kp.n_items, cap));
   if (flow) {
-    // items in 8 contiguous chunks, one per XCD (workgroup b takes tickets of chunk b % 8,
-    // round-robin placement puts it on XCD b % 8): consecutive items hand off inside one
-    // L2 except at 7 chunk seams.  Speed only: an item only waits on an earlier one and
-    // every workgroup is resident (one per CU, grid <= CUs), whatever the placement.
+    // Items go to the 8 XCDs in runs of G consecutive items, round-robin (workgroup b takes
+    // tickets of XCD b % 8 first, round-robin placement puts it there): a run hands off inside
+    // one L2.  When an XCD's share fits its workgroups (chunk <= CUs per XCD) the runs are 8
+    // contiguous chunks (7 seams).  A longer pair keeps more items in flight than an XCD has
+    // workgroups (97k: ~240 of 381 items at once, 32 CUs per XCD): contiguous chunks would then
+    // serialize -- chunk c + 1 waits for chunk c's last items, which wait for a free workgroup of
+    // XCD c (measured 28 ms for 97k x 97k) -- so the runs shrink to G = CUs per XCD / 8 and every
+    // XCD holds its share of the items in flight.  Speed only: an item only waits on an earlier
+    // one and every workgroup is resident (one per CU, grid <= CUs), whatever the placement.
     const int per_xcd = std::max(1, ncu / 8);
     const int chunk = (kp.n_items + 7) / 8;
-    kp.sched_cap = chunk;
+    kp.sched_cap = chunk <= per_xcd ? chunk : std::max(1, per_xcd / 8);  // G
     P->grid = 8 * std::max(1, std::min(chunk, per_xcd));
-    // two-pass: the remaining CUs run pass-2 blocks inside the same launch
+    // two-pass: the remaining CUs run pass-2 blocks inside the same launch, one flow workgroup per
+    // CU (the LDS floor): a pass-2 workgroup sharing a CU with a pass-1 one takes issue slots from its
+    // chain waves.  A long pair keeps ~n / (W lag) items in flight (97k: ~240), so pass 1 may hold
+    // most CUs; then every CU also gets a pass-2 workgroup (two per CU), whose waves issue at the
+    // lowest priority, behind the pass-1 waves (s_setprio, msa_flow.hip).  MSA_FLOW_LDS_MIN
+    // (bytes, diagnostic) overrides the one-per-CU floor.
     P->nflow = P->grid;
-    if (P->flow2) P->grid = std::max(P->grid + 8, 8 * per_xcd);
+    if (P->flow2) {
+      static const long lds_min = [] {
+        const char* e = std::getenv("MSA_FLOW_LDS_MIN");
+        return e ? std::strtol(e, nullptr, 10) : 80 * 1024 + 1024;
+      }();
+#ifndef FL_P2PERCU
+#define FL_P2PERCU 1  // pass-2 workgroups per CU beside the pass-1 one (long pairs)
+#endif
+      if (P->nflow > ncu / 2) {
+        P->grid = P->nflow + FL_P2PERCU * ncu;
+        // (LDS sized so that exactly FL_P2PERCU + 1 workgroups fit a CU, with room for its granularity)
+        P->lds_bytes = std::max(P->lds_bytes, ((size_t)(160 * 1024 / (FL_P2PERCU + 1)) & ~(size_t)4095) - 8192);
+      } else {
+        P->grid = std::max(P->grid + 8, 8 * per_xcd);
+        P->lds_bytes = std::max(P->lds_bytes, (size_t)std::max(0L, lds_min));
+      }
+      if (kernel_shape(P->fn, P->threads, P->lds_bytes) < 0) {
+        delete P;
+        return MSA_ERR_HIP;
+      }
+    }
   }
   // Banded single pair (C3-type): the band has only ~9 stripes in flight, so the exact
   // launch is one long chain of ~S x 8 phases.  Chunked mode runs it as n_chunks

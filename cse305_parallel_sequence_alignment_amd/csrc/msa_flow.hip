@@ -58,6 +58,7 @@ namespace msa {
 #ifndef FL_PS
 #define FL_PS 8         // phases per pass-2 segment (pass 1 saves its state every FL_PS phases)
 #endif
+#define FL_P2INTS 576   // LDS ints per pass-2 wave: two value streams (256 each) + the block's codes (64)
 #define FL_SPIN_MAX (1u << 26)  // a spin limit sets err = the site's code (10..15) instead of hanging
 #ifndef FL_PF
 #define FL_PF 12        // step of a phase at which the next phase's inputs are read
@@ -358,14 +359,28 @@ struct FillArgs {
   int oe;           // affine: gap_open - gap_extend (g = gap_extend); Gotoh: h
   msa_stripe_meta* meta;  // Gotoh: the final cell's tables go to the last stripe's meta
   int stripe0;
+#ifdef MSA_STAMPS
+  unsigned long long* stamps;  // diagnostic: pass-2 block tick totals (FL_P2STAT)
+#endif
 };
+#ifdef MSA_STAMPS
+// pass-2 totals (diagnostic build): [0] ticks waiting for the block's last granule, [1] ticks loading and
+// checking its inputs, [2] ticks computing + storing, [3] blocks, at item 62 / wave 15's stamp area
+#define FL_P2STAT(a_, k_, v_) \
+  do { if ((a_).stamps && lane == 0) atomicAdd((a_).stamps + ((size_t)(62 * 16 + 15) * 4096) * 4 + (k_), (unsigned long long)(v_)); } while (0)
+#else
+#define FL_P2STAT(a_, k_, v_) do {} while (0)
+#endif
 template <bool FLOOR, bool TRACKPOS, int R>
 __device__ __attribute__((noinline)) void fill_block(const FillArgs f, int blk, int lane, int* lds);
 __device__ __attribute__((noinline)) void fill_block_aff(const FillArgs f, int blk, int lane, int* lds);
 __device__ __attribute__((noinline)) void fill_block_got(const FillArgs f, int blk, int lane, int* lds);
 
 template <bool FLOOR, bool BEST, bool SAVE, bool TRACKPOS, int R = 1, int FK = 0>
-__global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
+#ifndef FL_WPE
+#define FL_WPE 2  // waves per SIMD the register budget is sized for (3: no faster for 97k pairs, C5 3% slower: spills)
+#endif
+__global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu(FL_WPE, 8))) void flow_kernel(KArgs a) {
   constexpr bool GS = !FLOOR;
   constexpr bool AFF = FK != 0;  // two values per link column (affine SW, Gotoh)
   constexpr bool GOT = FK == 2;  // the reference's Gotoh, tagged
@@ -391,7 +406,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
   const int g = kp.gap_ext;
   const int oe = kp.gap_open - kp.gap_ext;  // affine
   const unsigned ep = kp.epoch;
-  const int chunk = kp.sched_cap;
+  const int chunk = kp.sched_cap;  // G: items per XCD run (msa_plan_create)
 
 #ifdef MSA_STAMPS
   // workgroup lifetimes: item 63 / wave 15's area, q = blockIdx.x: slot 0 start, 1 end, 2 role
@@ -436,10 +451,14 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
         const FillArgs f{a.A, a.cod, a.br, a.snap, a.outH, a.blk, a.err, a.cod_copy, a.pairs[0].a_off,
                          a.pairs[0].cod_off, a.pairs[0].out_off, a.pairs[0].m, a.pairs[0].n, a.pairs[0].pmax,
                          a.nseg, a.brw, kp.match, kp.mismatch, kp.gap_ext, kp.epoch, a.outDir,
-                         kp.gap_open - kp.gap_ext, a.meta, a.pairs[0].stripe0};
-        if constexpr (GOT) fill_block_got(f, a.border[t], lane, smem + w * 544);
-        else if constexpr (AFF) fill_block_aff(f, a.border[t], lane, smem + w * 544);
-        else fill_block<FLOOR, TRACKPOS, R>(f, a.border[t], lane, smem + w * 544);
+                         kp.gap_open - kp.gap_ext, a.meta, a.pairs[0].stripe0
+#ifdef MSA_STAMPS
+                         , a.stamps
+#endif
+        };
+        if constexpr (GOT) fill_block_got(f, a.border[t], lane, smem + w * FL_P2INTS);
+        else if constexpr (AFF) fill_block_aff(f, a.border[t], lane, smem + w * FL_P2INTS);
+        else fill_block<FLOOR, TRACKPOS, R>(f, a.border[t], lane, smem + w * FL_P2INTS);
       }
 #ifdef MSA_STAMPS
       wg_stamp(1, __builtin_amdgcn_s_memrealtime());
@@ -447,18 +466,25 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
       return;
     }
   }
+  // pass-1 waves issue ahead of any pass-2 waves sharing their CU (long pairs: two workgroups per CU)
+#ifndef FL_P1PRIO
+#define FL_P1PRIO 3
+#endif
+  __builtin_amdgcn_s_setprio(FL_P1PRIO);
 
   for (;;) {
     if (threadIdx.x == 0) {
       // own chunk first, then the others': every item is claimed by a running
       // workgroup before any workgroup turns to pass-2 blocks (which wait on items)
+      // (XCD gg's t-th item: run t / G of its runs, which are runs gg, gg + 8, ... of G items)
       int it = kp.n_items;
       for (int d = 0; d < 8; ++d) {
         const int gg = (grp + d) & 7;
         if (gg * chunk >= kp.n_items) continue;
         const int t = atomicAdd(a.ticket + 4 + gg, 1);
-        if (t < chunk && gg * chunk + t < kp.n_items) {
-          it = gg * chunk + t;
+        const int x = ((t / chunk) * 8 + gg) * chunk + t % chunk;
+        if (x < kp.n_items) {
+          it = x;
           break;
         }
       }
@@ -1225,6 +1251,37 @@ __global__ __launch_bounds__((FL_W + 2) * 64) void flow_kernel(KArgs a) {
 #endif
 }
 
+// A pass-2 block's inputs are staged in its wave's LDS area (FL_P2INTS ints) before the phase loop:
+// the row above its FL_PS phases, value stream k at lds + 256 k (columns [0, nv) from the bottom-row
+// granules the caller loaded, row 0 for stripe 0, -inf past the producer's last block), and the column
+// codes the block reads -- columns cs - 63 + 16 q0 + [0, 256), one dword per lane from an aligned
+// staged copy -- at lds + 512.  The phase loop then issues no global load: a load in flight (codes
+// prefetched phases ahead) made every phase wait for the previous phases' H / direction stores too --
+// one vmcnt counter for both -- i.e. ~1 us per phase.  2.3 KiB per wave: pass-2 workgroups fit beside
+// a pass-1 one on a CU.
+template <int NV, class ROW0>
+__device__ __forceinline__ void p2_stage(int* lds, int s, int nv, int ntot, int lane, ROW0 row0, const uint8_t* cod,
+                                         long long cod_copy, int cs, int q0) {
+  const int b = cs - 63 + 16 * q0 - 1 + MSA_CPAD;  // byte of that first column in copy 0 (>= 0: CPAD 256)
+  const int c = b & (MSA_NCOPY - 1);              // copy c holds it at the 16-aligned byte b - c
+  const unsigned w = *reinterpret_cast<const unsigned*>(cod + (size_t)c * cod_copy + (b - c) + 4 * lane);
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
+    for (int v = (s == 0 ? 0 : nv) + lane; v < ntot; v += 64) *L(lds + 256 * k + v) = (s == 0) ? row0(v, k) : MSA_NEG;
+  *L(lds + 512 + lane) = (int)w;
+  FL_CBAR();  // (one wave's LDS ops execute in order: the phase loop's reads see these writes)
+}
+// Lane r's 16 column codes of the block's phase k (columns cs - r + 16 (q0 + k) + [0, 16)): five dwords
+// of the staged span and four byte-aligns (the shift (63 - r) mod 4 is the lane's for every phase).
+__device__ __forceinline__ fl_v4u p2_codes(int* lds, int k, int lane) {
+  const int o = (63 - lane) + 16 * k;
+  const lds_int* p = L(lds + 512 + (o >> 2));
+  const unsigned d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3], d4 = p[4];
+  const unsigned sh = (unsigned)o & 3u;
+  return fl_v4u{__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
+                __builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh)};
+}
+
 // Pass 2: block (stripe s, segment seg) of FL_PS phases, one wave.  Its inputs
 // are {epoch, value} granules that pass 1 may still be writing: the wave waits
 // for the block's last bottom-row granule, then loads and checks them all.
@@ -1288,12 +1345,9 @@ __device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, 
         if (lane == 0) atomicExch(a.err, 15);
         q1 = q0;  // nothing computed; the block reports no cell
       }
-      FL_CBAR();  // (one wave's LDS ops execute in order: the reads below see the writes)
-      // column codes: lane r needs columns cs - r + t; column c sits in global copy
-      // (c-1+CPAD)&15 at byte (c-1+CPAD) & ~15: one aligned dwordx4 per phase
-      const int b0 = cs - lane - 1 + MSA_CPAD;
-      const unsigned* cptr = reinterpret_cast<const unsigned*>(a.cod + (size_t)(b0 & (MSA_NCOPY - 1)) * a.cod_copy +
-                                                             a.cod_off + (b0 & ~(MSA_NCOPY - 1)));
+      // row 0 (stripe 0): H = 0 left of and on the top border
+      p2_stage<1>(lds, s, nv, 16 * (q1 - q0), lane,
+                  [&](int v, int) { return GS ? g * (cs + 16 * q0 + v) : -g; }, a.cod + a.cod_off, a.cod_copy, cs, q0);
       // H = G - g(i+j); i+j = 64Rs + 1 + cs + t + (R-1) lane on row 1, +1 on row 2
       const int negct0 = -g * (64 * R * s + 1 + cs + (R - 1) * lane);
       int gk[16];
@@ -1304,34 +1358,17 @@ __device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, 
       }
       int best = INT32_MIN, bt = -1, best2 = INT32_MIN, bt2 = -1;
       msa_v4i* hp = reinterpret_cast<msa_v4i*>(a.outH + (size_t)a.out_off + (size_t)s * a.pmax * MSA_K * 64 * R) + lane;
-      // column codes 4 phases ahead (one global dwordx4 per phase; ~1 us away otherwise)
-      auto ldc = [&](int q) __attribute__((always_inline)) {
-        return *reinterpret_cast<const uint4*>(cptr + 4 * min(q, P - 1));
-      };
-      uint4 cr0 = ldc(q0), cr1 = ldc(q0 + 1), cr2 = ldc(q0 + 2), cr3 = ldc(q0 + 3);
       for (int q = q0; q < q1; ++q) {
-        const uint4 c4 = cr0;
-        cr0 = cr1;
-        cr1 = cr2;
-        cr2 = cr3;
-        cr3 = ldc(q + 4);
         int IN[16];
-        if (q <= Bin) {
-          if (s == 0) {
+        {
+          const lds_int4* src = reinterpret_cast<const lds_int4*>(L(lds + 16 * (q - q0)));
 #pragma unroll
-            for (int j = 0; j < 16; ++j) IN[j] = GS ? g * (cs + 16 * q + j) : -g;
-          } else {
-            const lds_int4* src = reinterpret_cast<const lds_int4*>(L(lds + 16 * (q - q0)));
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const fl_v4i v = src[u];
-              IN[4 * u] = v.x; IN[4 * u + 1] = v.y; IN[4 * u + 2] = v.z; IN[4 * u + 3] = v.w;
-            }
+          for (int u = 0; u < 4; ++u) {
+            const fl_v4i v = src[u];
+            IN[4 * u] = v.x; IN[4 * u + 1] = v.y; IN[4 * u + 2] = v.z; IN[4 * u + 3] = v.w;
           }
-        } else {
-#pragma unroll
-          for (int j = 0; j < 16; ++j) IN[j] = MSA_NEG;
         }
+        const fl_v4u c4 = p2_codes(lds, q - q0, lane);
         const unsigned cw[4] = {c4.x, c4.y, c4.z, c4.w};
         const int negct = negct0 - 16 * g * q;
         int hv[16], hv2[16];
@@ -1463,45 +1500,26 @@ __device__ __attribute__((noinline)) void fill_block_aff(const FillArgs a, int b
         if (lane == 0) atomicExch(a.err, 15);
         q1 = q0;
       }
-      FL_CBAR();
-      const int b0 = cs - lane - 1 + MSA_CPAD;
-      const unsigned* cptr = reinterpret_cast<const unsigned*>(a.cod + (size_t)(b0 & (MSA_NCOPY - 1)) * a.cod_copy +
-                                                             a.cod_off + (b0 & ~(MSA_NCOPY - 1)));
+      // row 0 (stripe 0): Z = g col - oe (H = 0), F~ = -inf
+      p2_stage<2>(lds, s, nv, 16 * (q1 - q0), lane,
+                  [&](int v, int k) { return k == 0 ? g * (cs + 16 * q0 + v) - oe : MSA_NEG; }, a.cod + a.cod_off,
+                  a.cod_copy, cs, q0);
       const int flr0 = g * (64 * s + 1 + cs);
       int best = INT32_MIN, bt = -1;
       fl_v4u* dp = reinterpret_cast<fl_v4u*>(a.outDir + (size_t)a.out_off + (size_t)s * a.pmax * 1024) + lane;
-      auto ldc = [&](int q) __attribute__((always_inline)) {
-        return *reinterpret_cast<const uint4*>(cptr + 4 * min(q, P - 1));
-      };
-      uint4 cr0 = ldc(q0), cr1 = ldc(q0 + 1), cr2 = ldc(q0 + 2), cr3 = ldc(q0 + 3);
       for (int q = q0; q < q1; ++q) {
-        const uint4 c4 = cr0;
-        cr0 = cr1;
-        cr1 = cr2;
-        cr2 = cr3;
-        cr3 = ldc(q + 4);
         int INZ[16], INF[16];
-        if (q <= Bin) {
-          if (s == 0) {
+        {
+          const lds_int4* srz = reinterpret_cast<const lds_int4*>(L(lds + 16 * (q - q0)));
+          const lds_int4* srf = reinterpret_cast<const lds_int4*>(L(lds + 256 + 16 * (q - q0)));
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-              INZ[j] = g * (cs + 16 * q + j) - oe;
-              INF[j] = MSA_NEG;
-            }
-          } else {
-            const lds_int4* srz = reinterpret_cast<const lds_int4*>(L(lds + 16 * (q - q0)));
-            const lds_int4* srf = reinterpret_cast<const lds_int4*>(L(lds + 256 + 16 * (q - q0)));
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const fl_v4i vz = srz[u], vf = srf[u];
-              INZ[4 * u] = vz.x; INZ[4 * u + 1] = vz.y; INZ[4 * u + 2] = vz.z; INZ[4 * u + 3] = vz.w;
-              INF[4 * u] = vf.x; INF[4 * u + 1] = vf.y; INF[4 * u + 2] = vf.z; INF[4 * u + 3] = vf.w;
-            }
+          for (int u = 0; u < 4; ++u) {
+            const fl_v4i vz = srz[u], vf = srf[u];
+            INZ[4 * u] = vz.x; INZ[4 * u + 1] = vz.y; INZ[4 * u + 2] = vz.z; INZ[4 * u + 3] = vz.w;
+            INF[4 * u] = vf.x; INF[4 * u + 1] = vf.y; INF[4 * u + 2] = vf.z; INF[4 * u + 3] = vf.w;
           }
-        } else {
-#pragma unroll
-          for (int j = 0; j < 16; ++j) INZ[j] = INF[j] = MSA_NEG;
         }
+        const fl_v4u c4 = p2_codes(lds, q - q0, lane);
         const unsigned cw[4] = {c4.x, c4.y, c4.z, c4.w};
         const int flq = flr0 + 16 * g * q;
         unsigned dw[4];
@@ -1578,12 +1596,19 @@ __device__ __attribute__((noinline)) void fill_block_got(const FillArgs a, int b
       const int qb = (s > 0) ? min(q1, Bin + 1) : q0;
       const int nv = 16 * max(0, qb - q0);
       int Hs = 0, Rs = 0, Ds = 0, U = 0;
+#ifdef MSA_STAMPS
+      const unsigned long long tp0 = __builtin_amdgcn_s_memtime();
+      unsigned long long tp1 = tp0;
+#endif
       bool ready = (nv == 0);
       for (int t2 = 0; !ready && t2 < (int)(FL_SPIN_MAX >> 2); ++t2) {
         const unsigned long long gz = gload(brz + 16 * q0 + nv - 1), gf = gload(brf + 16 * q0 + nv - 1);
         ready = __ballot((unsigned)(gz >> 32) != ep || (unsigned)(gf >> 32) != ep) == 0;
         if (!ready) __builtin_amdgcn_s_sleep(FL_FSLEEP);
       }
+#ifdef MSA_STAMPS
+      tp1 = __builtin_amdgcn_s_memtime();
+#endif
       if (ready) {
         ready = false;
         for (int tries = 0; !ready && tries < (int)FL_SPIN_MAX; ++tries) {
@@ -1608,44 +1633,35 @@ __device__ __attribute__((noinline)) void fill_block_got(const FillArgs a, int b
         if (lane == 0) atomicExch(a.err, 15);
         q1 = q0;
       }
-      FL_CBAR();
-      const int b0 = cs - lane - 1 + MSA_CPAD;
-      const unsigned* cptr = reinterpret_cast<const unsigned*>(a.cod + (size_t)(b0 & (MSA_NCOPY - 1)) * a.cod_copy +
-                                                             a.cod_off + (b0 & ~(MSA_NCOPY - 1)));
+      // row 0 (stripe 0), tagged and shifted: H~ 3 at column 0, 2 - 4h right of it; D~ 3 - 4h, 2 - 8h
+      p2_stage<2>(lds, s, nv, 16 * (q1 - q0), lane,
+                  [&](int v, int k) {
+                    const int col = cs + 16 * q0 + v;
+                    return col < 0 ? MSA_NEG : (k == 0 ? (col == 0 ? 3 : 2 - h4) : (col == 0 ? 3 - h4 : 2 - 2 * h4));
+                  },
+                  a.cod + a.cod_off, a.cod_copy, cs, q0);
+#ifdef MSA_STAMPS
+      const unsigned long long tp2 = __builtin_amdgcn_s_memtime();
+#endif
       const int tmin = 1 - cs + lane;
       // the final cell (m, n): the lane of row m at step n - cs + lane of the last stripe
       const int tf = (row_i == m) ? n - cs + lane : -1;
       fl_v4u* dp = reinterpret_cast<fl_v4u*>(a.outDir + (size_t)a.out_off + (size_t)s * a.pmax * 1024) + lane;
-      auto ldc = [&](int q) __attribute__((always_inline)) {
-        return *reinterpret_cast<const uint4*>(cptr + 4 * min(q, P - 1));
-      };
-      uint4 cr0 = ldc(q0), cr1 = ldc(q0 + 1), cr2 = ldc(q0 + 2), cr3 = ldc(q0 + 3);
-      auto phase = [&](const int q, const uint4 c4, auto HEAD_, auto CAP_) __attribute__((always_inline)) {
+      auto phase = [&](const int q, auto HEAD_, auto CAP_) __attribute__((always_inline)) {
         constexpr bool HEAD = decltype(HEAD_)::value;  // lanes left of column 1 hold the border
         constexpr bool CAP = decltype(CAP_)::value;    // the phase holds cell (m, n)
         int INZ[16], INF[16];
-        if (q <= Bin) {
-          if (s == 0) {
+        {
+          const lds_int4* srz = reinterpret_cast<const lds_int4*>(L(lds + 16 * (q - q0)));
+          const lds_int4* srf = reinterpret_cast<const lds_int4*>(L(lds + 256 + 16 * (q - q0)));
 #pragma unroll
-            for (int jj = 0; jj < 16; ++jj) {
-              const int col = cs + 16 * q + jj;
-              INZ[jj] = col < 0 ? MSA_NEG : (col == 0 ? 3 : 2 - h4);
-              INF[jj] = col < 0 ? MSA_NEG : (col == 0 ? 3 - h4 : 2 - 2 * h4);
-            }
-          } else {
-            const lds_int4* srz = reinterpret_cast<const lds_int4*>(L(lds + 16 * (q - q0)));
-            const lds_int4* srf = reinterpret_cast<const lds_int4*>(L(lds + 256 + 16 * (q - q0)));
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const fl_v4i vz = srz[u], vf = srf[u];
-              INZ[4 * u] = vz.x; INZ[4 * u + 1] = vz.y; INZ[4 * u + 2] = vz.z; INZ[4 * u + 3] = vz.w;
-              INF[4 * u] = vf.x; INF[4 * u + 1] = vf.y; INF[4 * u + 2] = vf.z; INF[4 * u + 3] = vf.w;
-            }
+          for (int u = 0; u < 4; ++u) {
+            const fl_v4i vz = srz[u], vf = srf[u];
+            INZ[4 * u] = vz.x; INZ[4 * u + 1] = vz.y; INZ[4 * u + 2] = vz.z; INZ[4 * u + 3] = vz.w;
+            INF[4 * u] = vf.x; INF[4 * u + 1] = vf.y; INF[4 * u + 2] = vf.z; INF[4 * u + 3] = vf.w;
           }
-        } else {
-#pragma unroll
-          for (int jj = 0; jj < 16; ++jj) INZ[jj] = INF[jj] = MSA_NEG;
         }
+        const fl_v4u c4 = p2_codes(lds, q - q0, lane);
         const unsigned cw[4] = {c4.x, c4.y, c4.z, c4.w};
         unsigned dw[4];
 #pragma unroll
@@ -1696,16 +1712,20 @@ __device__ __attribute__((noinline)) void fill_block_got(const FillArgs a, int b
       using T_ = std::true_type;
       using F_ = std::false_type;
       for (int q = q0; q < q1; ++q) {
-        const uint4 c4 = cr0;
-        cr0 = cr1;
-        cr1 = cr2;
-        cr2 = cr3;
-        cr3 = ldc(q + 4);
         const bool cap = __ballot(tf >= 16 * q && tf < 16 * q + 16) != 0ull;
-        if (cap) phase(q, c4, T_{}, T_{});
-        else if (q < 6) phase(q, c4, T_{}, F_{});
-        else phase(q, c4, F_{}, F_{});
+        if (cap) phase(q, T_{}, T_{});
+        else if (q < 6) phase(q, T_{}, F_{});
+        else phase(q, F_{}, F_{});
       }
+#ifdef MSA_STAMPS
+      const unsigned long long tp3 = __builtin_amdgcn_s_memtime();
+      if ((blk & 15) == 0) {  // a sample of the blocks (the atomics would serialize all of them)
+        FL_P2STAT(a, 0, tp1 - tp0);
+        FL_P2STAT(a, 1, tp2 - tp1);
+        FL_P2STAT(a, 2, tp3 - tp2);
+        FL_P2STAT(a, 3, 1);
+      }
+#endif
     }
   }
   if (lane == 0) a.blk[blk] = make_int4(0, 0, 0, 0);

@@ -22,6 +22,8 @@ from cse305_parallel_sequence_alignment_amd.plan import Plan
 ap = argparse.ArgumentParser()
 ap.add_argument("--workload", default="c2", choices=["c2", "c5", "ref"])
 ap.add_argument("--tag", default="")
+ap.add_argument("--ref-len", type=int, default=10000, help="ref: prefix length (0 = whole sequences)")
+ap.add_argument("--ref-pair", default="0,1")
 args = ap.parse_args()
 wl = args.workload
 if wl == "c2":
@@ -36,7 +38,10 @@ elif wl == "c5":
     out = torch.empty(pl.cells_elems, dtype=torch.uint8, device="cuda")
     rows = 64
 else:
-    A, B = data.bundled()[0][:10000], data.bundled()[1][:10000]
+    ia, ib = (int(x) for x in args.ref_pair.split(","))
+    A, B = data.bundled()[ia], data.bundled()[ib]
+    if args.ref_len:
+        A, B = A[:args.ref_len], B[:args.ref_len]
     pl = Plan(LB.REF_GOTOH, LB.CELLS_DIR, [len(A)], [len(B)], [0], [0], match=1, mismatch=0, gap_open=3,
               gap_extend=1, start_type=-1)
     out = torch.empty(pl.cells_elems, dtype=torch.uint8, device="cuda")
@@ -105,4 +110,9 @@ if claimed.any():
     io0 = full[0, 4, 0, 0]
     if io0:
         out.update(item0_codes_loaded_us=round(float((io0 - t0) / 100.0), 2))
+p2 = full[62, 15, 0, :]  # pass-2 block totals (Gotoh fill blocks): wait, load, compute ticks, blocks
+if p2[3]:
+    out.update(p2_blocks=int(p2[3]), p2_wait_ticks_per_block=round(float(p2[0]) / p2[3], 1),
+               p2_load_ticks_per_block=round(float(p2[1]) / p2[3], 1),
+               p2_compute_ticks_per_block=round(float(p2[2]) / p2[3], 1))
 print(json.dumps(out), flush=True)
