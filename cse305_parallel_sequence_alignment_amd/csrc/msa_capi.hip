@@ -326,7 +326,8 @@ kfn_t pick_flow(int alg, bool best, bool save, int tp, int R, bool nneg) {
     if (!save || R != 1) return nullptr;
     return nneg ? flow_kernel<false, false, true, true, 1, 1> : flow_kernel<true, false, true, true, 1, 1>;
   }
-  if (alg == MSA_ALG_REF1) return (save && R == 1) ? flow_kernel<true, false, true, true, 1, 2> : nullptr;
+  if (alg == MSA_ALG_REF1)
+    return !save ? nullptr : (R == 2 ? flow_kernel<true, false, true, true, 2, 2> : flow_kernel<true, false, true, true, 1, 2>);
   // score-only plans: pass 1 alone, one row per lane, best cell tracked in the chain;
   // H plans: pass 1 + in-launch pass 2, two rows per lane
   const bool fl = (alg == MSA_ALG_SWL);
@@ -336,6 +337,15 @@ kfn_t pick_flow(int alg, bool best, bool save, int tp, int R, bool nneg) {
     return tp ? flow_kernel<false, false, true, true, 2> : flow_kernel<false, false, true, false, 2>;
   }
   return nullptr;
+}
+
+// the separate pass-2 launch of a long pair (flow_fill_kernel), same instantiation parameters
+kfn_t pick_fill(int alg, int tp, int R, bool nneg) {
+  if (alg == MSA_ALG_SWA) return nneg ? flow_fill_kernel<false, false, 1, 1> : flow_fill_kernel<true, false, 1, 1>;
+  if (alg == MSA_ALG_REF1) return R == 2 ? flow_fill_kernel<true, false, 2, 2> : flow_fill_kernel<true, false, 1, 2>;
+  if (R != 2) return nullptr;
+  if (alg == MSA_ALG_SWL) return tp ? flow_fill_kernel<true, true, 2, 0> : flow_fill_kernel<true, false, 2, 0>;
+  return tp ? flow_fill_kernel<false, true, 2, 0> : flow_fill_kernel<false, false, 2, 0>;
 }
 
 }  // namespace
@@ -354,6 +364,9 @@ struct msa_plan {
   int threads = 64;
   bool flow = false;   // flow_kernel (single-pair SW linear) instead of stripe_kernel
   bool flow2 = false;  // + pass-2 blocks inside the same launch (O_H)
+  kfn_t fill_fn = nullptr;  // long pairs: pass 2 as a launch of its own behind pass 1
+  int fill_grid = 0;
+  size_t fill_lds = 0;
   unsigned long long* d_br = nullptr;
   unsigned long long* d_snap = nullptr;
   int4* d_blk = nullptr;
@@ -557,7 +570,12 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   P->KS = KS;
   P->threads = (flow ? W + 2 : W + 1 + (single ? 1 : 0)) * 64;
   // rows per lane of the flow kernel (two-pass plans): 2 halves the inter-wave hand-offs per row
-  P->R = (flow && out_mode == MSA_OUT_H) ? 2 : 1;
+  // (SW linear with H; the reference's Gotoh with direction bytes, MSA_FLOW_GOT_R=1 keeps one row)
+  static const int got_r = [] {
+    const char* e = std::getenv("MSA_FLOW_GOT_R");
+    return (e && std::atoi(e) == 1) ? 1 : 2;
+  }();
+  P->R = (flow && (out_mode == MSA_OUT_H || kalg == MSA_ALG_REF1)) ? (kalg == MSA_ALG_REF1 ? got_r : 2) : 1;
   P->fn = flow ? pick_flow(kalg, out_mode == MSA_OUT_NONE, P->flow2, tp, P->R, desc->match >= 0 && desc->mismatch >= 0)
                : pick_kernel(kalg, out_mode, tp, single);
   if (!P->fn) { delete P; return MSA_ERR_UNSUPPORTED; }
@@ -736,13 +754,17 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
         const char* e = std::getenv("MSA_FLOW_LDS_MIN");
         return e ? std::strtol(e, nullptr, 10) : 80 * 1024 + 1024;
       }();
-#ifndef FL_P2PERCU
-#define FL_P2PERCU 1  // pass-2 workgroups per CU beside the pass-1 one (long pairs)
-#endif
       if (P->nflow > ncu / 2) {
-        P->grid = P->nflow + FL_P2PERCU * ncu;
-        // (LDS sized so that exactly FL_P2PERCU + 1 workgroups fit a CU, with room for its granularity)
-        P->lds_bytes = std::max(P->lds_bytes, ((size_t)(160 * 1024 / (FL_P2PERCU + 1)) & ~(size_t)4095) - 8192);
+        // pass 1 holds most CUs: pass 2 runs as a launch of its own behind it (flow_fill_kernel), whose
+        // register budget is the pass-2 code's alone (97k x 97k: 23 -> ~16 ms)
+        P->grid = P->nflow;
+        P->fill_fn = pick_fill(kalg, tp, P->R, desc->match >= 0 && desc->mismatch >= 0);
+        if (!P->fill_fn) { delete P; return MSA_ERR_UNSUPPORTED; }
+        P->fill_lds = (size_t)FL_FILLW * FL_P2INTS * 4;
+        const int focc = kernel_shape(P->fill_fn, FL_FILLW * 64, P->fill_lds);
+        if (focc < 0) { delete P; return MSA_ERR_HIP; }
+        P->fill_grid = ncu * std::max(1, std::min(focc, 8));
+        P->lds_bytes = std::max(P->lds_bytes, (size_t)std::max(0L, lds_min));
       } else {
         P->grid = std::max(P->grid + 8, 8 * per_xcd);
         P->lds_bytes = std::max(P->lds_bytes, (size_t)std::max(0L, lds_min));
@@ -851,7 +873,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     // (affine: the F~ bottom rows follow the Z rows; a snapshot is 4 values per lane)
     const bool two = P->kp.alg == MSA_ALG_SWA || P->kp.alg == MSA_ALG_REF1;
     const size_t brb = sizeof(unsigned long long) * (size_t)S * P->brw * (two ? 2 : 1);
-    const size_t snb = sizeof(unsigned long long) * (size_t)P->nblk * (two ? 256 : 128 * P->R);
+    const size_t snb = sizeof(unsigned long long) * (size_t)P->nblk * (two ? 128 * (P->R + 1) : 128 * P->R);
     if (!P->alloc(&P->d_br, brb) || hipMemset(P->d_br, 0, brb) != hipSuccess) return fail();
     if (!P->alloc(&P->d_snap, snb) || hipMemset(P->d_snap, 0, snb) != hipSuccess) return fail();
     if (!P->alloc(&P->d_blk, sizeof(int4) * (size_t)P->nblk)) return fail();
@@ -983,6 +1005,10 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
     hipLaunchKernelGGL(P->fb_fn, dim3(P->fb_grid), dim3(P->fb_threads), P->fb_lds, st, b);
     HIPCHK(hipGetLastError());
   }
+  if (P->fill_fn) {  // long pair: pass 2 behind pass 1
+    hipLaunchKernelGGL(P->fill_fn, dim3(P->fill_grid), dim3(FL_FILLW * 64), P->fill_lds, st, a);
+    HIPCHK(hipGetLastError());
+  }
   if (ev) HIPCHK(hipEventRecord(P->ev1, st));
   if (P->flow2 && P->kp.alg != MSA_ALG_REF1) {  // (Gotoh: the final state is in the last stripe's meta)
     hipLaunchKernelGGL(reduce_blocks_kernel, dim3(1), dim3(1024), 0, st, (const int4*)P->d_blk, P->nblk, P->d_res);
@@ -1103,7 +1129,8 @@ int msa_plan_traceback_gotoh(msa_plan* P, int64_t pair, int end_type, const uint
   hipStream_t st = (hipStream_t)stream;
   P->note_stream(st);
   // REF1 bytes hold tags (3 / 2 / 1 = T1 / T2 / T3), REF bytes the table numbers
-  hipLaunchKernelGGL(P->kp.alg == MSA_ALG_REF1 ? traceback_kernel<TB_REF_TAG> : traceback_kernel<TB_REF>, dim3(1),
+  hipLaunchKernelGGL(P->kp.alg == MSA_ALG_REF1 ? (P->R == 2 ? traceback_kernel<TB_REF_TAG, 2> : traceback_kernel<TB_REF_TAG>)
+                                               : traceback_kernel<TB_REF>, dim3(1),
                      dim3(64), 0, st, dDir, P->d_pairs, P->d_meta, (const PairResult*)P->d_res, (int)pair, end_type,
                      (int)P->kp.h, d_ops, (long long)ops_cap, (long long*)d_info, P->flow ? 1 : 0);
   HIPCHK(hipGetLastError());

@@ -59,6 +59,7 @@ namespace msa {
 #define FL_PS 8         // phases per pass-2 segment (pass 1 saves its state every FL_PS phases)
 #endif
 #define FL_P2INTS 576   // LDS ints per pass-2 wave: two value streams (256 each) + the block's codes (64)
+#define FL_FILLW 4      // waves per workgroup of the separate pass-2 launch (flow_fill_kernel)
 #define FL_SPIN_MAX (1u << 26)  // a spin limit sets err = the site's code (10..15) instead of hanging
 #ifndef FL_PF
 #define FL_PF 12        // step of a phase at which the next phase's inputs are read
@@ -108,6 +109,7 @@ typedef int fl_v4i __attribute__((ext_vector_type(4)));
 typedef unsigned fl_v4u __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) fl_v4i lds_int4;
 __device__ __forceinline__ lds_int* L(int* p) { return (lds_int*)(p); }
+__device__ __forceinline__ lds_int* L(lds_int* p) { return p; }
 __device__ __forceinline__ int lds_vload(const int* p) { return *(volatile lds_int*)(p); }
 __device__ __forceinline__ void lds_vstore(int* p, int v) { *(volatile lds_int*)(p) = v; }
 #define FL_CBAR() asm volatile("" ::: "memory")
@@ -371,10 +373,26 @@ struct FillArgs {
 #else
 #define FL_P2STAT(a_, k_, v_) do {} while (0)
 #endif
+// Pass-2 block functions read their arguments from the kernel's own argument segment (scalar loads,
+// FillArgs built in SGPRs) and get their wave's LDS area as an LDS pointer: no by-value struct on the
+// stack, so the kernel needs no scratch (a stack copy of FillArgs per call cost the launch its scratch
+// setup and every access a private-memory load).
+typedef const __attribute__((address_space(4))) struct KArgs kargs_c;
+__device__ __forceinline__ FillArgs fill_args_of(kargs_c* k) {
+  const msa_pair_desc pd = k->pairs[0];
+  return FillArgs{k->A, k->cod, k->br, k->snap, k->outH, k->blk, k->err, k->cod_copy, pd.a_off, pd.cod_off,
+                  pd.out_off, pd.m, pd.n, pd.pmax, k->nseg, k->brw, k->kp.match, k->kp.mismatch, k->kp.gap_ext,
+                  k->kp.epoch, k->outDir, k->kp.gap_open - k->kp.gap_ext, k->meta, pd.stripe0
+#ifdef MSA_STAMPS
+                  , k->stamps
+#endif
+  };
+}
 template <bool FLOOR, bool TRACKPOS, int R>
-__device__ __attribute__((noinline)) void fill_block(const FillArgs f, int blk, int lane, int* lds);
-__device__ __attribute__((noinline)) void fill_block_aff(const FillArgs f, int blk, int lane, int* lds);
-__device__ __attribute__((noinline)) void fill_block_got(const FillArgs f, int blk, int lane, int* lds);
+__device__ __attribute__((noinline)) void fill_block(kargs_c* ka, int blk, int lane, lds_int* lds);
+__device__ __attribute__((noinline)) void fill_block_aff(kargs_c* ka, int blk, int lane, lds_int* lds);
+__device__ __attribute__((noinline)) void fill_block_got(kargs_c* ka, int blk, int lane, lds_int* lds);
+__device__ __attribute__((noinline)) void fill_block_got2(kargs_c* ka, int blk, int lane, lds_int* lds);
 
 template <bool FLOOR, bool BEST, bool SAVE, bool TRACKPOS, int R = 1, int FK = 0>
 #ifndef FL_WPE
@@ -385,7 +403,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
   constexpr bool AFF = FK != 0;  // two values per link column (affine SW, Gotoh)
   constexpr bool GOT = FK == 2;  // the reference's Gotoh, tagged
   static_assert(R == 1 || (R == 2 && !BEST), "two rows per lane: pass-2 plans only");
-  static_assert(!AFF || (R == 1 && SAVE && !BEST), "affine: two-pass, one row per lane");
+  static_assert(!AFF || ((R == 1 || GOT) && SAVE && !BEST), "affine: two-pass, one row per lane; Gotoh: R = 1 or 2");
   constexpr int NV = AFF ? 2 : 1;                  // values per column on a link (Z, F~)
   constexpr int NCP = AFF ? 4 : FL_NCOPY;          // LDS code copies (affine: 4-byte aligned reads)
   extern __shared__ __attribute__((aligned(16))) int smem[];
@@ -448,17 +466,12 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
         if (lane == 0) t = atomicAdd(a.ticket + MSA_TK_BLOCK, 1);
         t = __builtin_amdgcn_readlane(t, 0);
         if (t >= a.nblk) break;
-        const FillArgs f{a.A, a.cod, a.br, a.snap, a.outH, a.blk, a.err, a.cod_copy, a.pairs[0].a_off,
-                         a.pairs[0].cod_off, a.pairs[0].out_off, a.pairs[0].m, a.pairs[0].n, a.pairs[0].pmax,
-                         a.nseg, a.brw, kp.match, kp.mismatch, kp.gap_ext, kp.epoch, a.outDir,
-                         kp.gap_open - kp.gap_ext, a.meta, a.pairs[0].stripe0
-#ifdef MSA_STAMPS
-                         , a.stamps
-#endif
-        };
-        if constexpr (GOT) fill_block_got(f, a.border[t], lane, smem + w * FL_P2INTS);
-        else if constexpr (AFF) fill_block_aff(f, a.border[t], lane, smem + w * FL_P2INTS);
-        else fill_block<FLOOR, TRACKPOS, R>(f, a.border[t], lane, smem + w * FL_P2INTS);
+        kargs_c* ka = (kargs_c*)__builtin_amdgcn_kernarg_segment_ptr();  // (a is the only argument)
+        lds_int* wl = L(smem + w * FL_P2INTS);
+        if constexpr (GOT && R == 2) fill_block_got2(ka, a.border[t], lane, wl);
+        else if constexpr (GOT) fill_block_got(ka, a.border[t], lane, wl);
+        else if constexpr (AFF) fill_block_aff(ka, a.border[t], lane, wl);
+        else fill_block<FLOOR, TRACKPOS, R>(ka, a.border[t], lane, wl);
       }
 #ifdef MSA_STAMPS
       wg_stamp(1, __builtin_amdgcn_s_memrealtime());
@@ -697,11 +710,12 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
       // =================== compute wave (affine / Gotoh): stripe k ===================
       const int k = k0 + w;
       const int cs = fl_cs(k);
-      const int P = fl_P(k, m, n, 1);
-      const int row_i = 64 * k + lane + 1;
+      const int P = fl_P(k, m, n, R);
+      const int row_i = 64 * R * k + R * lane + 1;  // (R = 2, Gotoh: rows row_i, row_i + 1)
       const unsigned ac = (row_i <= m) ? (a.A[pd.a_off + row_i - 1] & 7u) : 0u;
+      const unsigned ac2 = (R == 2 && row_i + 1 <= m) ? (a.A[pd.a_off + row_i] & 7u) : 0u;
       const bool has_out = (k < S - 1);
-      const int Bin = (k == 0) ? P - 1 : min(P - 1, fl_bmax(k, m, n, 1));
+      const int Bin = (k == 0) ? P - 1 : min(P - 1, fl_bmax(k, m, n, R));
       const int dq_in = (w == 0) ? 0 : fl_dq(k);
       const int dq = has_out ? fl_dq(k + 1) : 0;
       const unsigned a_ring_in = lds_addr(rings + w * 512);
@@ -711,9 +725,10 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
       const unsigned a_prog_me = lds_addr(prog_me);
       const unsigned a_cons1 = lds_addr(w + 1 < W ? flags + 32 + w + 2 : flags + 64 + W);
       const unsigned a_cons2 = lds_addr(flags + 64 + w + 1);
-      unsigned plo, phi;
+      unsigned plo, phi, plo2 = 0, phi2 = 0;
       if constexpr (GOT) fl_profile_got(g, ac, plo, phi);
       else fl_profile_aff(kp.match, kp.mismatch, g, oe, ac, plo, phi);
+      if constexpr (R == 2) fl_profile_got(g, ac2, plo2, phi2);
       // LDS code address of phase q: ring of copy x, byte (y_lane + 16 q) mod FL_CRING
       unsigned a_cring, y_code;
       {
@@ -735,6 +750,10 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
         Fo = 1;
         U = MSA_NEG;
       }
+      // R = 2 (Gotoh): row 2's H~, R~ + 4h and D~ + 4h (Zl / E / U hold row 1's; row 2's diagonal is
+      // row 1's previous H~, its cell above row 1's new one -- no state of their own); the next lane's
+      // row 1 takes the cell above from row 2 (Zl2, Fo2) through the DPP
+      int Zl2 = 1 - 4 * oe, E2 = 1 - 4 * oe, Fo2 = 1;
       int pubv = 0, consv = 0;
       unsigned spins = 0;
       fl_v4i ZA[4], FA[4], ZB[4], FB[4];
@@ -820,11 +839,21 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
           if constexpr (MASK) mask_in(q, Z, F);
         }
         if (q % FL_PS == 0) {  // pass 2 restarts here: each lane's (Z left, E~, F~, diagonal Z)
-          unsigned long long* sp = a.snap + ((size_t)k * a.nseg + q / FL_PS) * 256 + lane;
-          gstore(sp, ((unsigned long long)ep << 32) | (unsigned)Zl);
-          gstore(sp + 64, ((unsigned long long)ep << 32) | (unsigned)(GOT ? E - 4 * oe : E));  // pass 2: R~, D~
-          gstore(sp + 128, ((unsigned long long)ep << 32) | (unsigned)(GOT ? Fo - 4 * oe : Fo));
-          gstore(sp + 192, ((unsigned long long)ep << 32) | (unsigned)U);
+          if constexpr (R == 2) {  // rows 1 and 2: H~, R~, diagonal H~ / H~, R~, D~ (pass 2: unshifted)
+            unsigned long long* sp = a.snap + ((size_t)k * a.nseg + q / FL_PS) * 384 + lane;
+            gstore(sp, ((unsigned long long)ep << 32) | (unsigned)Zl);
+            gstore(sp + 64, ((unsigned long long)ep << 32) | (unsigned)(E - 4 * oe));
+            gstore(sp + 128, ((unsigned long long)ep << 32) | (unsigned)U);
+            gstore(sp + 192, ((unsigned long long)ep << 32) | (unsigned)Zl2);
+            gstore(sp + 256, ((unsigned long long)ep << 32) | (unsigned)(E2 - 4 * oe));
+            gstore(sp + 320, ((unsigned long long)ep << 32) | (unsigned)(Fo2 - 4 * oe));
+          } else {
+            unsigned long long* sp = a.snap + ((size_t)k * a.nseg + q / FL_PS) * 256 + lane;
+            gstore(sp, ((unsigned long long)ep << 32) | (unsigned)Zl);
+            gstore(sp + 64, ((unsigned long long)ep << 32) | (unsigned)(GOT ? E - 4 * oe : E));  // pass 2: R~, D~
+            gstore(sp + 128, ((unsigned long long)ep << 32) | (unsigned)(GOT ? Fo - 4 * oe : Fo));
+            gstore(sp + 192, ((unsigned long long)ep << 32) | (unsigned)U);
+          }
         }
         int xz[16], xf[16];
         int pubn = 0;
@@ -833,12 +862,58 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const unsigned s4 = __builtin_amdgcn_perm(phi, plo, cw[u]);
+          const unsigned s4b = (R == 2) ? __builtin_amdgcn_perm(phi2, plo2, cw[u]) : 0u;
 #pragma unroll
           for (int kk = 0; kk < 4; ++kk) {
             const int kx = 4 * u + kk;
             if (kx == FL_PF) issue_reads(q + 1, Zn, Fn, Cln, Chn, pubn);
             const int sc = ((int)(s4 << (24 - 8 * kk))) >> 24;
-            if constexpr (GOT) {
+            if constexpr (GOT && R == 2) {
+              // row 1: the cell above is the previous lane's row 2 (lane 0: the link)
+              const int uH = dpp_shr1(Z[kx >> 2][kx & 3], Zl2);
+              const int uD = dpp_shr1(F[kx >> 2][kx & 3], Fo2);
+              const int t1 = (int)((unsigned)U | 3u) + sc;
+              const int t2p = (int)(((unsigned)E & ~3u) | 2u);
+              const int t3p = (int)(((unsigned)uD & ~3u) | 1u);
+              const int t2 = t2p - 4 * oe, t3 = t3p - 4 * oe;
+              int h1 = imax3(t1, t2, t3);
+              int rr1 = imax3(t1, t2p, t3);
+              int dd1 = imax3(t1, t2, t3p);
+              asm("" : "+v"(h1));
+              // row 2: diagonal = row 1's previous H~, above = row 1's new cell
+              const int sb = ((int)(s4b << (24 - 8 * kk))) >> 24;
+              const int s1 = (int)((unsigned)Zl | 3u) + sb;
+              const int s2p = (int)(((unsigned)E2 & ~3u) | 2u);
+              const int s2 = s2p - 4 * oe;
+              int h2, rr2, dd2;
+              if constexpr (HEAD) {
+                const bool before = 16 * q + kx < tmin;
+                h1 = before ? 1 - 4 * oe : h1;
+                rr1 = before ? 1 - 4 * oe : rr1;
+                dd1 = before ? 1 : dd1;
+                const int s3p = (int)(((unsigned)dd1 & ~3u) | 1u), s3 = s3p - 4 * oe;
+                h2 = imax3(s1, s2, s3);
+                rr2 = imax3(s1, s2p, s3);
+                dd2 = imax3(s1, s2, s3p);
+                h2 = before ? 1 - 4 * oe : h2;
+                rr2 = before ? 1 - 4 * oe : rr2;
+                dd2 = before ? 1 : dd2;
+              } else {
+                const int s3p = (int)(((unsigned)dd1 & ~3u) | 1u), s3 = s3p - 4 * oe;
+                h2 = imax3(s1, s2, s3);
+                rr2 = imax3(s1, s2p, s3);
+                dd2 = imax3(s1, s2, s3p);
+              }
+              asm("" : "+v"(h2));
+              U = uH;
+              Zl = h1;
+              E = rr1;
+              Zl2 = h2;
+              E2 = rr2;
+              Fo2 = dd2;
+              xz[kx] = h2;
+              xf[kx] = dd2;
+            } else if constexpr (GOT) {
               // R~ and D~ are carried + 4h (E = R~ + 4h, Fo / F = D~ + 4h): then
               //   R~ + 4h = max3(t1, t2 + 4h, t3),  D~ + 4h = max3(t1, t2, t3 + 4h)
               // and t2 = t2' - 4h, t3 = t3' - 4h (4h keeps the tag bits): 11 VALU per step, not 12.
@@ -1260,7 +1335,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
 // one vmcnt counter for both -- i.e. ~1 us per phase.  2.3 KiB per wave: pass-2 workgroups fit beside
 // a pass-1 one on a CU.
 template <int NV, class ROW0>
-__device__ __forceinline__ void p2_stage(int* lds, int s, int nv, int ntot, int lane, ROW0 row0, const uint8_t* cod,
+__device__ __forceinline__ void p2_stage(lds_int* lds, int s, int nv, int ntot, int lane, ROW0 row0, const uint8_t* cod,
                                          long long cod_copy, int cs, int q0) {
   const int b = cs - 63 + 16 * q0 - 1 + MSA_CPAD;  // byte of that first column in copy 0 (>= 0: CPAD 256)
   const int c = b & (MSA_NCOPY - 1);              // copy c holds it at the 16-aligned byte b - c
@@ -1273,7 +1348,7 @@ __device__ __forceinline__ void p2_stage(int* lds, int s, int nv, int ntot, int 
 }
 // Lane r's 16 column codes of the block's phase k (columns cs - r + 16 (q0 + k) + [0, 16)): five dwords
 // of the staged span and four byte-aligns (the shift (63 - r) mod 4 is the lane's for every phase).
-__device__ __forceinline__ fl_v4u p2_codes(int* lds, int k, int lane) {
+__device__ __forceinline__ fl_v4u p2_codes(lds_int* lds, int k, int lane) {
   const int o = (63 - lane) + 16 * k;
   const lds_int* p = L(lds + 512 + (o >> 2));
   const unsigned d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3], d4 = p[4];
@@ -1288,7 +1363,8 @@ __device__ __forceinline__ fl_v4u p2_codes(int* lds, int k, int lane) {
 // R = 2: lane r holds rows 128s+2r+1 (X/U) and 128s+2r+2 (X2); cells go to the
 // R = 2 layout (per 4 steps: the wave's row-1 int4s, then its row-2 int4s).
 template <bool FLOOR, bool TRACKPOS, int R>
-__device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, int lane, int* lds) {
+__device__ __attribute__((noinline)) void fill_block(kargs_c* ka, int blk, int lane, lds_int* lds) {
+  const FillArgs a = fill_args_of(ka);
   constexpr bool GS = !FLOOR;
   const unsigned ep = a.ep;
   const int m = a.m, n = a.n, S = (m + 64 * R - 1) / (64 * R), g = a.g;
@@ -1444,7 +1520,8 @@ __device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, 
 // phase are one 16-byte store, a wave's phase one contiguous 1 KiB -- and reduces its first
 // maximum H = H~ - e(i+j).  The bytes are stripe_kernel's MSA_ALG_SWA bytes (the walk
 // traceback_kernel<TB_SW> reads them unchanged).
-__device__ __attribute__((noinline)) void fill_block_aff(const FillArgs a, int blk, int lane, int* lds) {
+__device__ __attribute__((noinline)) void fill_block_aff(kargs_c* ka, int blk, int lane, lds_int* lds) {
+  const FillArgs a = fill_args_of(ka);
   const unsigned ep = a.ep;
   const int m = a.m, n = a.n, S = (m + 63) / 64, g = a.g, oe = a.oe;
   const int s = blk / a.nseg, seg = blk - s * a.nseg;
@@ -1575,7 +1652,8 @@ __device__ __attribute__((noinline)) void fill_block_aff(const FillArgs a, int b
 // layout.  The block holding cell (m, n) stores its three tables, unshifted, as the last
 // stripe's final state (reduce_pairs_kernel turns it into the pair result, the walk reads
 // find_alignment's end rule from it).
-__device__ __attribute__((noinline)) void fill_block_got(const FillArgs a, int blk, int lane, int* lds) {
+__device__ __attribute__((noinline)) void fill_block_got(kargs_c* ka, int blk, int lane, lds_int* lds) {
+  const FillArgs a = fill_args_of(ka);
   const unsigned ep = a.ep;
   const int m = a.m, n = a.n, S = (m + 63) / 64, g = a.g, h4 = 4 * a.oe;
   const int s = blk / a.nseg, seg = blk - s * a.nseg;
@@ -1729,6 +1807,203 @@ __device__ __attribute__((noinline)) void fill_block_got(const FillArgs a, int b
     }
   }
   if (lane == 0) a.blk[blk] = make_int4(0, 0, 0, 0);
+}
+
+// Pass 2, Gotoh, two rows per lane (R = 2: 128-row stripes, lane r holds rows 128s+2r+1 and
+// 128s+2r+2 at column cs + t - r): as fill_block_got, both rows per step -- row 1 takes the cell above
+// from the previous lane's row 2 (lane 0: the stripe above's bottom row), row 2 from row 1 at the same
+// column, its diagonal from row 1's previous cell.  A phase's bytes go out as one 2 KiB block: the
+// wave's row-1 16-byte segments, then its row-2 segments (traceback_kernel's R = 2 layout).
+__device__ __attribute__((noinline)) void fill_block_got2(kargs_c* ka, int blk, int lane, lds_int* lds) {
+  const FillArgs a = fill_args_of(ka);
+  const unsigned ep = a.ep;
+  const int m = a.m, n = a.n, S = (m + 127) / 128, g = a.g, h4 = 4 * a.oe;
+  const int s = blk / a.nseg, seg = blk - s * a.nseg;
+  if (s < S) {
+    const int P = fl_P(s, m, n, 2);
+    const int q0 = seg * FL_PS;
+    if (q0 < P) {
+      int q1 = min(P, q0 + FL_PS);
+      const int cs = fl_cs(s);
+      const int row_i = 128 * s + 2 * lane + 1;
+      const unsigned ac = (row_i <= m) ? (a.A[a.a_off + row_i - 1] & 7u) : 0u;
+      const unsigned ac2 = (row_i + 1 <= m) ? (a.A[a.a_off + row_i] & 7u) : 0u;
+      unsigned plo, phi, plo2, phi2;
+      fl_profile_got(g, ac, plo, phi);
+      fl_profile_got(g, ac2, plo2, phi2);
+      const int Bin = (s == 0) ? P - 1 : min(P - 1, fl_bmax(s, m, n, 2));
+      const unsigned long long* sp = a.snap + ((size_t)s * a.nseg + seg) * 384 + lane;
+      const unsigned long long* brz = a.br + (size_t)(s > 0 ? s - 1 : 0) * a.brw;
+      const unsigned long long* brf = a.br + (size_t)(S + (s > 0 ? s - 1 : 0)) * a.brw;
+      const int qb = (s > 0) ? min(q1, Bin + 1) : q0;
+      const int nv = 16 * max(0, qb - q0);
+      int U = 0, Hs1 = 0, Rs1 = 0, Hs2 = 0, Rs2 = 0, Ds2 = 0;
+      bool ready = (nv == 0);
+      for (int t2 = 0; !ready && t2 < (int)(FL_SPIN_MAX >> 2); ++t2) {
+        const unsigned long long gz = gload(brz + 16 * q0 + nv - 1), gf = gload(brf + 16 * q0 + nv - 1);
+        ready = __ballot((unsigned)(gz >> 32) != ep || (unsigned)(gf >> 32) != ep) == 0;
+        if (!ready) __builtin_amdgcn_s_sleep(FL_FSLEEP);
+      }
+      if (ready) {
+        ready = false;
+        for (int tries = 0; !ready && tries < (int)FL_SPIN_MAX; ++tries) {
+          const unsigned long long x0 = gload(sp), x1 = gload(sp + 64), x2 = gload(sp + 128), x3 = gload(sp + 192),
+                                   x4 = gload(sp + 256), x5 = gload(sp + 320);
+          bool ok = ((unsigned)(x0 >> 32) == ep) && ((unsigned)(x1 >> 32) == ep) && ((unsigned)(x2 >> 32) == ep) &&
+                    ((unsigned)(x3 >> 32) == ep) && ((unsigned)(x4 >> 32) == ep) && ((unsigned)(x5 >> 32) == ep);
+          Hs1 = (int)(unsigned)x0;
+          Rs1 = (int)(unsigned)x1;
+          U = (int)(unsigned)x2;
+          Hs2 = (int)(unsigned)x3;
+          Rs2 = (int)(unsigned)x4;
+          Ds2 = (int)(unsigned)x5;
+          for (int v = lane; v < nv; v += 64) {
+            const unsigned long long gz = gload(brz + 16 * q0 + v), gf = gload(brf + 16 * q0 + v);
+            ok = ok && ((unsigned)(gz >> 32) == ep) && ((unsigned)(gf >> 32) == ep);
+            *L(lds + v) = (int)(unsigned)gz;
+            *L(lds + 256 + v) = (int)(unsigned)gf;
+          }
+          ready = __ballot(!ok) == 0;
+          if (!ready) __builtin_amdgcn_s_sleep(8);
+        }
+      }
+      if (!ready) {
+        if (lane == 0) atomicExch(a.err, 15);
+        q1 = q0;
+      }
+      // row 0 (stripe 0), tagged and shifted: H~ 3 at column 0, 2 - 4h right of it; D~ 3 - 4h, 2 - 8h
+      p2_stage<2>(lds, s, nv, 16 * (q1 - q0), lane,
+                  [&](int v, int k) {
+                    const int col = cs + 16 * q0 + v;
+                    return col < 0 ? MSA_NEG : (k == 0 ? (col == 0 ? 3 : 2 - h4) : (col == 0 ? 3 - h4 : 2 - 2 * h4));
+                  },
+                  a.cod + a.cod_off, a.cod_copy, cs, q0);
+      const int tmin = 1 - cs + lane;
+      // the final cell (m, n): row m is row 1 or row 2 of one lane of the last stripe
+      const int tf1 = (row_i == m) ? n - cs + lane : -1;
+      const int tf2 = (row_i + 1 == m) ? n - cs + lane : -1;
+      const int tf = max(tf1, tf2);
+      fl_v4u* dp = reinterpret_cast<fl_v4u*>(a.outDir + (size_t)a.out_off + (size_t)s * a.pmax * 2048) + lane;
+      auto phase = [&](const int q, auto HEAD_, auto CAP_) __attribute__((always_inline)) {
+        constexpr bool HEAD = decltype(HEAD_)::value;  // lanes left of column 1 hold the border
+        constexpr bool CAP = decltype(CAP_)::value;    // the phase holds cell (m, n)
+        int INZ[16], INF[16];
+        {
+          const lds_int4* srz = reinterpret_cast<const lds_int4*>(L(lds + 16 * (q - q0)));
+          const lds_int4* srf = reinterpret_cast<const lds_int4*>(L(lds + 256 + 16 * (q - q0)));
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const fl_v4i vz = srz[u], vf = srf[u];
+            INZ[4 * u] = vz.x; INZ[4 * u + 1] = vz.y; INZ[4 * u + 2] = vz.z; INZ[4 * u + 3] = vz.w;
+            INF[4 * u] = vf.x; INF[4 * u + 1] = vf.y; INF[4 * u + 2] = vf.z; INF[4 * u + 3] = vf.w;
+          }
+        }
+        const fl_v4u c4 = p2_codes(lds, q - q0, lane);
+        const unsigned cw[4] = {c4.x, c4.y, c4.z, c4.w};
+        unsigned dw1[4], dw2[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const unsigned s4 = __builtin_amdgcn_perm(phi, plo, cw[u]);
+          const unsigned s4b = __builtin_amdgcn_perm(phi2, plo2, cw[u]);
+          unsigned word1 = 0, word2 = 0;
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) {
+            const int kx = 4 * u + kk;
+            const int sc = ((int)(s4 << (24 - 8 * kk))) >> 24;
+            const int sb = ((int)(s4b << (24 - 8 * kk))) >> 24;
+            // row 1
+            const int uH = dpp_shr1(INZ[kx], Hs2);
+            const int uD = dpp_shr1(INF[kx], Ds2);
+            const int t1 = (int)((unsigned)U | 3u) + sc;
+            const int t2 = (int)(((unsigned)Rs1 & ~3u) | 2u);
+            const int t3 = (int)(((unsigned)uD & ~3u) | 1u);
+            word1 |= (((unsigned)U & 3u) | (((unsigned)Rs1 & 3u) << 2) | (((unsigned)uD & 3u) << 4)) << (8 * kk);
+            const int t1h = t1 - h4;
+            int hh1 = imax3(t1, t2, t3);
+            int rr1 = imax3(t1h, t2, t3 - h4);
+            int dd1 = imax3(t1h, t2 - h4, t3);
+            asm("" : "+v"(hh1));
+            // row 2: diagonal = row 1's previous H~, above = row 1's new cell
+            const bool before = HEAD && (16 * q + kx < tmin);
+            if constexpr (HEAD) {
+              hh1 = before ? 1 - h4 : hh1;
+              rr1 = before ? 1 - 2 * h4 : rr1;
+              dd1 = before ? 1 - h4 : dd1;
+            }
+            const int s1 = (int)((unsigned)Hs1 | 3u) + sb;
+            const int s2 = (int)(((unsigned)Rs2 & ~3u) | 2u);
+            const int s3 = (int)(((unsigned)dd1 & ~3u) | 1u);
+            word2 |= (((unsigned)Hs1 & 3u) | (((unsigned)Rs2 & 3u) << 2) | (((unsigned)dd1 & 3u) << 4)) << (8 * kk);
+            const int s1h = s1 - h4;
+            int hh2 = imax3(s1, s2, s3);
+            int rr2 = imax3(s1h, s2, s3 - h4);
+            int dd2 = imax3(s1h, s2 - h4, s3);
+            asm("" : "+v"(hh2));
+            if constexpr (HEAD) {
+              hh2 = before ? 1 - h4 : hh2;
+              rr2 = before ? 1 - 2 * h4 : rr2;
+              dd2 = before ? 1 - h4 : dd2;
+            }
+            if constexpr (CAP) {
+              if (16 * q + kx == tf) {
+                const int gmn = g * (m + n);  // unshift
+                // (the slot reduce_pairs_kernel reads: the last 64-row stripe's meta)
+                msa_stripe_meta* md = a.meta + a.stripe0 + (m + 63) / 64 - 1;
+                md->fin[0] = ((tf1 >= 0 ? t1 : s1) >> 2) - gmn;
+                md->fin[1] = ((tf1 >= 0 ? t2 : s2) >> 2) - gmn;
+                md->fin[2] = ((tf1 >= 0 ? t3 : s3) >> 2) - gmn;
+                md->has_fin = 1;
+              }
+            }
+            U = uH;
+            Hs1 = hh1;
+            Rs1 = rr1;
+            Hs2 = hh2;
+            Rs2 = rr2;
+            Ds2 = dd2;
+          }
+          dw1[u] = word1;
+          dw2[u] = word2;
+        }
+        __builtin_nontemporal_store(fl_v4u{dw1[0], dw1[1], dw1[2], dw1[3]}, dp + (size_t)q * 128);
+        __builtin_nontemporal_store(fl_v4u{dw2[0], dw2[1], dw2[2], dw2[3]}, dp + (size_t)q * 128 + 64);
+      };
+      using T_ = std::true_type;
+      using F_ = std::false_type;
+      for (int q = q0; q < q1; ++q) {
+        const bool cap = __ballot(tf >= 16 * q && tf < 16 * q + 16) != 0ull;
+        if (cap) phase(q, T_{}, T_{});
+        else if (q < 6) phase(q, T_{}, F_{});
+        else phase(q, F_{}, F_{});
+      }
+    }
+  }
+  if (lane == 0) a.blk[blk] = make_int4(0, 0, 0, 0);
+}
+
+// Pass 2 as a launch of its own, queued behind the pass-1 launch, for long pairs (msa_plan_create:
+// pass 1 needs most CUs -- ~n / (W lag) items in flight -- and the flow kernel's register budget
+// (~220 VGPRs for affine / Gotoh) leaves no room for a pass-2 workgroup beside a pass-1 one, so
+// in-launch pass-2 workgroups only started once pass 1 was done, at 1.5 waves per SIMD).  Here
+// every input is complete when the blocks start, and the pass-2 code alone sets the register
+// budget: several waves per SIMD hide each other's LDS and store latency.
+template <bool FLOOR, bool TRACKPOS, int R, int FK>
+__global__ __launch_bounds__(FL_FILLW * 64) void flow_fill_kernel(KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) int smem[];
+  const int lane = threadIdx.x & 63;
+  const int w = uni(threadIdx.x >> 6);
+  kargs_c* ka = (kargs_c*)__builtin_amdgcn_kernarg_segment_ptr();  // (a is the only argument)
+  lds_int* wl = L(smem + w * FL_P2INTS);
+  for (;;) {
+    int t = 0;
+    if (lane == 0) t = atomicAdd(a.ticket + MSA_TK_BLOCK, 1);
+    t = __builtin_amdgcn_readlane(t, 0);
+    if (t >= a.nblk) break;
+    if constexpr (FK == 2 && R == 2) fill_block_got2(ka, a.border[t], lane, wl);
+    else if constexpr (FK == 2) fill_block_got(ka, a.border[t], lane, wl);
+    else if constexpr (FK == 1) fill_block_aff(ka, a.border[t], lane, wl);
+    else fill_block<FLOOR, TRACKPOS, R>(ka, a.border[t], lane, wl);
+  }
 }
 
 // Pair result of a two-pass plan from the pass-2 block bests: every thread folds

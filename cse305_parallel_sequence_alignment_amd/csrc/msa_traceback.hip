@@ -163,8 +163,10 @@ __device__ __forceinline__ bool tb_diag_stay(unsigned dv) {
 }
 
 // KIND TB_SW: Smith-Waterman affine walk; TB_REF / TB_REF_TAG: the reference's Gotoh walk
-// (end_type, h: find_alignment's end rule).
-template <int KIND>
+// (end_type, h: find_alignment's end rule).  RL = rows per lane of the layout: 1, or 2 for the
+// two-rows-per-lane Gotoh flow fill (128-row stripes, lane r holds rows 2r+1 and 2r+2 at column
+// cs + t - r; a 16-step block is 2 KiB: the row-1 segments, then the row-2 segments).
+template <int KIND, int RL = 1>
 __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict__ dir,
                                                        const msa_pair_desc* __restrict__ pairs,
                                                        const msa_stripe_meta* __restrict__ meta,
@@ -186,16 +188,17 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
   int status = 0;
   // Group slots: 4 x 16 KiB behind a guard (window lanes whose cell lies outside the group
   // read an unused byte there -- down to 2,270 B below a slot -- and hold frozen words).
-  constexpr int GB = 16, GT = 16 * GB, GBYTES = 1024 * GB, NSLOT = 4;
+  constexpr int GB = 16, GT = 16 * GB, GBYTES = 1024 * RL * GB, NSLOT = 4;
+  constexpr int SR = 64 * RL;  // rows per stripe
   constexpr int TB_GUARD = 2304;
   __shared__ __attribute__((aligned(16))) uint8_t stage_raw[TB_GUARD + NSLOT * GBYTES];
   typedef __attribute__((address_space(3))) uint8_t lds_u8;
   const unsigned stage_lds = (unsigned)(uintptr_t)(lds_u8*)&stage_raw[TB_GUARD];
   // every stripe's start column, staged in LDS once (a stripe change then costs an LDS
   // read, not a ~1 us dependent global load); pairs with more stripes read the rest from HBM
-  constexpr int TB_CSL = 8192;
+  constexpr int TB_CSL = RL == 1 ? 8192 : 1;  // (RL = 2: flow layouts only, stripe starts computed)
   __shared__ int csl[TB_CSL];
-  const int S = (pd.m + 63) / 64;
+  const int S = (pd.m + SR - 1) / SR;
   if (!csflow)
     for (int k = lane; k < S && k < TB_CSL; k += 64) csl[k] = meta[pd.stripe0 + k].cs;
   auto cs_of = [&](int k) {  // wave-uniform (readfirstlane: an LDS value is otherwise "divergent")
@@ -275,14 +278,18 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
   auto stage_group = [&](int s, int b0) __attribute__((always_inline)) {
     const int k = s & (NSLOT - 1);
     const unsigned dst = stage_lds + (unsigned)GBYTES * (unsigned)k;
-    const uint8_t* g = base + ((long long)s * pmax + b0) * 1024;
+    const uint8_t* g = base + ((long long)s * pmax + b0) * (1024 * RL);
     if (pmax >= GB) {
       glds16x16(g, dst);
+      if constexpr (RL == 2) glds16x16(g + 16384, dst + 16384u);
     } else {
 #pragma unroll
-      for (int q = 0; q < GB; ++q) glds16(base + ((long long)s * pmax + (q < pmax ? q : pmax - 1)) * 1024, dst + 1024u * q);
+      for (int q = 0; q < GB * RL; ++q) {
+        const int qb = q / RL < pmax ? q / RL : pmax - 1;  // (a short stripe loads its last block again)
+        glds16(base + ((long long)s * pmax + qb) * (1024 * RL) + 1024 * (q % RL), dst + 1024u * q);
+      }
     }
-    issued += GB;
+    issued += GB * RL;
     set4(k, s, slot_s0, slot_s1, slot_s2, slot_s3);
     set4(k, b0, slot_b0, slot_b1, slot_b2, slot_b3);
     set4(k, issued, slot_e0, slot_e1, slot_e2, slot_e3);
@@ -312,14 +319,14 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
     int s_cur = -1, cs = 0;
     // outer iteration: the walk entered a stripe, or left its group on the left
     while (i > 0 && j > 0 && !stopped) {
-      const int s = (i - 1) >> 6;
-      int r = (i - 1) & 63;
+      const int s = (i - 1) / SR;
+      int r = (i - 1) - SR * s;  // row in the stripe (RL = 2: lane r >> 1, half r & 1)
       const bool entered = s != s_cur;
       if (entered) {
         cs = cs_of(s);
         s_cur = s;
       }
-      const int t = j - cs + r;
+      const int t = j - cs + (RL == 2 ? (r >> 1) : r);
       const int k = s & (NSLOT - 1);
       int b0 = sel4(k, slot_b0, slot_b1, slot_b2, slot_b3);
       if (!entered || sel4(k, slot_s0, slot_s1, slot_s2, slot_s3) != s || t < 16 * b0 || t >= 16 * b0 + GT) {
@@ -350,7 +357,8 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
           const int sd = s - d;
           if (sd < 0) break;
           if (sel4(sd & (NSLOT - 1), slot_s0, slot_s1, slot_s2, slot_s3) == sd) continue;
-          stage_group(sd, group_b0(j - r - 64 * d + 126 - cs_of(sd)));
+          // (RL = 2: it enters row 128 (s - d) + 128, lane 63, at column j - r - 128 d + 127)
+          stage_group(sd, group_b0(RL == 2 ? j - r - 128 * d + 190 - cs_of(sd) : j - r - 64 * d + 126 - cs_of(sd)));
         }
       }
       const unsigned grp_lds = stage_lds + (unsigned)GBYTES * (unsigned)k;
@@ -368,9 +376,15 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
           int qmax = r < (tg >> 1) ? r : (tg >> 1);
           qmax = qmax < i - 1 ? qmax : i - 1;
           qmax = qmax < j - 1 ? qmax : j - 1;
-          const bool valid = lane <= qmax;
-          const int tt = tg - 2 * lane, rr = r - lane;
-          const unsigned ga = grp_lds + (valid ? (unsigned)(((tt >> 4) << 10) + (rr << 4) + (tt & 15)) : 0u);
+          bool valid = lane <= qmax;
+          int tt = tg - 2 * lane, rr = r - lane;
+          unsigned go = (unsigned)(((tt >> 4) << 10) + (rr << 4) + (tt & 15));
+          if constexpr (RL == 2) {  // cell (i - q, j - q): step t - q - (r/2 - rr/2), 2 KiB blocks
+            tt = tg - lane - ((r >> 1) - (rr >> 1));
+            valid = lane <= min(min(r, i - 1), j - 1) && tt >= 0;
+            go = (unsigned)(((tt >> 4) << 11) + ((rr & 1) << 10) + ((rr >> 1) << 4) + (tt & 15));
+          }
+          const unsigned ga = grp_lds + (valid ? go : 0u);
           const unsigned dv = *(const lds_u8*)(uintptr_t)ga;
           const unsigned long long bal = __ballot(valid && tb_diag_stay<KIND>(dv));
           const int q = ~bal == 0ull ? 64 : (int)__builtin_ctzll(~bal);  // leading "diagonal, stay" cells
@@ -379,8 +393,9 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
 #endif
           if (q > 0) {
             record((15u << 28) | (unsigned)q);
+            if constexpr (RL == 2) tg -= q + ((r >> 1) - ((r - q) >> 1));
+            else tg -= 2 * q;
             r -= q;
-            tg -= 2 * q;
             i -= q;
             j -= q;
             if (r < 0 || tg < 0 || i <= 0 || j <= 0) break;
@@ -389,10 +404,18 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
         // a window of seven steps
         int wt;
         {
-          const int d = (tg & 15) - wc;
-          const unsigned ga = grp_lds + (unsigned)(((tg >> 4) << 10) + (r << 4)) + (unsigned)(d + 1008 * (d >> 4) - wa16);
+          unsigned ga;
+          bool live;
+          if constexpr (RL == 2) {  // lane (a, b): cell (i - a, j - b), row r - a, step tg - b - (r/2 - (r-a)/2)
+            const int rr = r - wa, tt = tg - wb - ((r >> 1) - (rr >> 1));
+            live = wa <= min(r, i - 1) && wb <= j - 1 && tt >= 0;
+            ga = grp_lds + (live ? (unsigned)(((tt >> 4) << 11) + ((rr & 1) << 10) + ((rr >> 1) << 4) + (tt & 15)) : 0u);
+          } else {
+            const int d = (tg & 15) - wc;
+            ga = grp_lds + (unsigned)(((tg >> 4) << 10) + (r << 4)) + (unsigned)(d + 1008 * (d >> 4) - wa16);
+            live = wa <= min(r, i - 1) && wb <= j - 1 && wc <= tg;
+          }
           const unsigned dv = *(const lds_u8*)(uintptr_t)ga;
-          const bool live = wa <= min(r, i - 1) && wb <= j - 1 && wc <= tg;
           const unsigned w = tb_word<KIND>(dv);  // (evaluated for every lane: a select, no branch)
           wt = (int)(live ? w : FROZEN);
         }
@@ -412,8 +435,9 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
         sh &= 31;
         record(wcode | (7u << 28));
         const int da = idx >> 3, db = idx & 7;
+        if constexpr (RL == 2) tg -= db + ((r >> 1) - ((r - da) >> 1));
+        else tg -= da + db;
         r -= da;
-        tg -= da + db;
         i -= da;
         j -= db;
 #ifdef MSA_TB_STATS

@@ -249,21 +249,25 @@ class Plan:
         return out
 
     def deskew_dir(self, flat: np.ndarray, pair: int, meta: np.ndarray) -> np.ndarray:
+        """Row-major (m+1) x (n+1) matrix of a pair's direction bytes.  Two rows per lane (the Gotoh flow
+        fill): a 16-step block is 2 KiB, the wave's row-1 segments then its row-2 segments."""
         g = self.geom[pair]
-        S = (g.m + 63) // 64
-        blk = flat[g.out_off:g.out_off + S * g.pmax * 1024].reshape(S, g.pmax, 64, 16)
+        R = g.rows_per_lane
+        S = (g.m + 64 * R - 1) // (64 * R)
+        blk = flat[g.out_off:g.out_off + S * g.pmax * 1024 * R].reshape(S, g.pmax, R, 64, 16)
         out = np.zeros((g.m + 1, g.n + 1), dtype=np.uint8)
         T = g.pmax * 16
         t = np.arange(T)
         r = np.arange(64)
         for s in range(S):
             cs = int(meta[g.stripe0 + s, 0])
-            vals = blk[s].transpose(1, 0, 2).reshape(64, T)
-            i = 64 * s + r + 1
             j = cs + t[None, :] - r[:, None]
-            ok = (i[:, None] <= g.m) & (j >= 1) & (j <= g.n)
-            ii = np.broadcast_to(i[:, None], j.shape)
-            out[ii[ok], j[ok]] = vals[ok]
+            for rho in range(R):
+                vals = blk[s, :, rho].transpose(1, 0, 2).reshape(64, T)
+                i = 64 * R * s + R * r + rho + 1
+                ok = (i[:, None] <= g.m) & (j >= 1) & (j <= g.n)
+                ii = np.broadcast_to(i[:, None], j.shape)
+                out[ii[ok], j[ok]] = vals[ok]
         return out
 
 

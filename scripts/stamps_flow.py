@@ -88,7 +88,7 @@ out = dict(tag=args.tag, workload=wl, kernel_ms=[round(x, 4) for x in kms], stri
            wait_in_ticks_mean=float(np.mean([wq[r[0] // 4, r[0] % 4, 0] for r in recs])),
            wait_cons_ticks_mean=float(np.mean([wq[r[0] // 4, r[0] % 4, 1] for r in recs])),
            ncons_mean=float(np.mean([wq[r[0] // 4, r[0] % 4, 2] for r in recs])))
-wg = full[63, 15, :, :]
+wg = full[63, 15, :2048, :]
 started = wg[:, 0] > 0
 if started.any():
     ws, we, role = wg[started, 0], wg[started, 1], wg[started, 2]
@@ -96,7 +96,10 @@ if started.any():
                wg_last_end_us=round(float((we.max() - t0) / 100.0), 2),
                pass1_last_end_us=round(float((we[role == 1].max() - t0) / 100.0), 2) if (role == 1).any() else None,
                pass2_last_end_us=round(float((we[role == 2].max() - t0) / 100.0), 2) if (role == 2).any() else None,
-               wg_last_start_us=round(float((ws.max() - t0) / 100.0), 2))
+               wg_last_start_us=round(float((ws.max() - t0) / 100.0), 2),
+               wg_started_after_100us=int(((ws - t0) / 100.0 > 100).sum()),
+               wg_pass1=int((role == 1).sum()), wg_pass2=int((role == 2).sum()),
+               pass2_started_after_100us=int((((ws - t0) / 100.0) > 100)[role == 2].sum()))
 cl = full[63, 15, 2048:, :]
 claimed = cl[:, 2] > 0
 if claimed.any():
