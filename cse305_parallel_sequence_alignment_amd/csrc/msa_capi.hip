@@ -323,7 +323,8 @@ kfn_t pick_flow(int alg, bool best, bool save, int tp, int R, bool nneg) {
   // SW affine / the reference's Gotoh (direction bytes): pass 1 + in-launch pass 2, one row per lane;
   // SW affine with scores >= 0: pass 1 applies the zero floor in its head phases only
   if (alg == MSA_ALG_SWA) {
-    if (!save || R != 1) return nullptr;
+    if (!save) return nullptr;
+    if (R == 2) return nneg ? flow_kernel<false, false, true, true, 2, 1> : flow_kernel<true, false, true, true, 2, 1>;
     return nneg ? flow_kernel<false, false, true, true, 1, 1> : flow_kernel<true, false, true, true, 1, 1>;
   }
   if (alg == MSA_ALG_REF1)
@@ -341,7 +342,9 @@ kfn_t pick_flow(int alg, bool best, bool save, int tp, int R, bool nneg) {
 
 // the separate pass-2 launch of a long pair (flow_fill_kernel), same instantiation parameters
 kfn_t pick_fill(int alg, int tp, int R, bool nneg) {
-  if (alg == MSA_ALG_SWA) return nneg ? flow_fill_kernel<false, false, 1, 1> : flow_fill_kernel<true, false, 1, 1>;
+  if (alg == MSA_ALG_SWA)
+    return R == 2 ? (nneg ? flow_fill_kernel<false, false, 2, 1> : flow_fill_kernel<true, false, 2, 1>)
+                  : (nneg ? flow_fill_kernel<false, false, 1, 1> : flow_fill_kernel<true, false, 1, 1>);
   if (alg == MSA_ALG_REF1) return R == 2 ? flow_fill_kernel<true, false, 2, 2> : flow_fill_kernel<true, false, 1, 2>;
   if (R != 2) return nullptr;
   if (alg == MSA_ALG_SWL) return tp ? flow_fill_kernel<true, true, 2, 0> : flow_fill_kernel<true, false, 2, 0>;
@@ -570,12 +573,17 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   P->KS = KS;
   P->threads = (flow ? W + 2 : W + 1 + (single ? 1 : 0)) * 64;
   // rows per lane of the flow kernel (two-pass plans): 2 halves the inter-wave hand-offs per row
-  // (SW linear with H; the reference's Gotoh with direction bytes, MSA_FLOW_GOT_R=1 keeps one row)
+  // (SW linear with H; the reference's Gotoh and SW affine with direction bytes; MSA_FLOW_GOT_R=1 /
+  // MSA_FLOW_AFF_R=1 keep one row for those two)
   static const int got_r = [] {
     const char* e = std::getenv("MSA_FLOW_GOT_R");
     return (e && std::atoi(e) == 1) ? 1 : 2;
   }();
-  P->R = (flow && (out_mode == MSA_OUT_H || kalg == MSA_ALG_REF1)) ? (kalg == MSA_ALG_REF1 ? got_r : 2) : 1;
+  static const int aff_r = [] {
+    const char* e = std::getenv("MSA_FLOW_AFF_R");
+    return (e && std::atoi(e) == 1) ? 1 : 2;
+  }();
+  P->R = !flow ? 1 : kalg == MSA_ALG_REF1 ? got_r : kalg == MSA_ALG_SWA ? aff_r : (out_mode == MSA_OUT_H ? 2 : 1);
   P->fn = flow ? pick_flow(kalg, out_mode == MSA_OUT_NONE, P->flow2, tp, P->R, desc->match >= 0 && desc->mismatch >= 0)
                : pick_kernel(kalg, out_mode, tp, single);
   if (!P->fn) { delete P; return MSA_ERR_UNSUPPORTED; }
@@ -1113,7 +1121,7 @@ int msa_plan_traceback(msa_plan* P, int64_t pair, const uint8_t* dDir, uint8_t* 
   if (P->kp.alg != MSA_ALG_SWA || P->d.cells != MSA_CELLS_DIR || !P->d.track_end) return MSA_ERR_UNSUPPORTED;
   hipStream_t st = (hipStream_t)stream;
   P->note_stream(st);
-  hipLaunchKernelGGL(traceback_kernel<TB_SW>, dim3(1), dim3(64), 0, st, dDir, P->d_pairs, P->d_meta,
+  hipLaunchKernelGGL((P->R == 2 ? traceback_kernel<TB_SW, 2> : traceback_kernel<TB_SW>), dim3(1), dim3(64), 0, st, dDir, P->d_pairs, P->d_meta,
                      (const PairResult*)P->d_res, (int)pair, 0, 0, d_ops, (long long)ops_cap, (long long*)d_info,
                      P->flow ? 1 : 0);
   HIPCHK(hipGetLastError());

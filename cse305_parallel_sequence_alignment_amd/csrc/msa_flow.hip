@@ -391,6 +391,7 @@ __device__ __forceinline__ FillArgs fill_args_of(kargs_c* k) {
 template <bool FLOOR, bool TRACKPOS, int R>
 __device__ __attribute__((noinline)) void fill_block(kargs_c* ka, int blk, int lane, lds_int* lds);
 __device__ __attribute__((noinline)) void fill_block_aff(kargs_c* ka, int blk, int lane, lds_int* lds);
+__device__ __attribute__((noinline)) void fill_block_aff2(kargs_c* ka, int blk, int lane, lds_int* lds);
 __device__ __attribute__((noinline)) void fill_block_got(kargs_c* ka, int blk, int lane, lds_int* lds);
 __device__ __attribute__((noinline)) void fill_block_got2(kargs_c* ka, int blk, int lane, lds_int* lds);
 
@@ -403,7 +404,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
   constexpr bool AFF = FK != 0;  // two values per link column (affine SW, Gotoh)
   constexpr bool GOT = FK == 2;  // the reference's Gotoh, tagged
   static_assert(R == 1 || (R == 2 && !BEST), "two rows per lane: pass-2 plans only");
-  static_assert(!AFF || ((R == 1 || GOT) && SAVE && !BEST), "affine: two-pass, one row per lane; Gotoh: R = 1 or 2");
+  static_assert(!AFF || (SAVE && !BEST), "affine / Gotoh: two-pass");
   constexpr int NV = AFF ? 2 : 1;                  // values per column on a link (Z, F~)
   constexpr int NCP = AFF ? 4 : FL_NCOPY;          // LDS code copies (affine: 4-byte aligned reads)
   extern __shared__ __attribute__((aligned(16))) int smem[];
@@ -470,6 +471,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
         lds_int* wl = L(smem + w * FL_P2INTS);
         if constexpr (GOT && R == 2) fill_block_got2(ka, a.border[t], lane, wl);
         else if constexpr (GOT) fill_block_got(ka, a.border[t], lane, wl);
+        else if constexpr (AFF && R == 2) fill_block_aff2(ka, a.border[t], lane, wl);
         else if constexpr (AFF) fill_block_aff(ka, a.border[t], lane, wl);
         else fill_block<FLOOR, TRACKPOS, R>(ka, a.border[t], lane, wl);
       }
@@ -728,7 +730,8 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
       unsigned plo, phi, plo2 = 0, phi2 = 0;
       if constexpr (GOT) fl_profile_got(g, ac, plo, phi);
       else fl_profile_aff(kp.match, kp.mismatch, g, oe, ac, plo, phi);
-      if constexpr (R == 2) fl_profile_got(g, ac2, plo2, phi2);
+      if constexpr (R == 2 && GOT) fl_profile_got(g, ac2, plo2, phi2);
+      if constexpr (R == 2 && !GOT) fl_profile_aff(kp.match, kp.mismatch, g, oe, ac2, plo2, phi2);
       // LDS code address of phase q: ring of copy x, byte (y_lane + 16 q) mod FL_CRING
       unsigned a_cring, y_code;
       {
@@ -752,8 +755,15 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
       }
       // R = 2 (Gotoh): row 2's H~, R~ + 4h and D~ + 4h (Zl / E / U hold row 1's; row 2's diagonal is
       // row 1's previous H~, its cell above row 1's new one -- no state of their own); the next lane's
-      // row 1 takes the cell above from row 2 (Zl2, Fo2) through the DPP
+      // row 1 takes the cell above from row 2 (Zl2, Fo2) through the DPP.  Affine: row 2's Z left, E~,
+      // F~ (virtual cells left of column 1: H = 0, Z = e(i+j) - oe), the lane's floor e(i+j) row 1
       int Zl2 = 1 - 4 * oe, E2 = 1 - 4 * oe, Fo2 = 1;
+      const int flb = g * (128 * k + 1 + cs + lane);  // affine R = 2: e(i+j) of row 1 at step 0
+      if constexpr (R == 2 && !GOT) {
+        Zl2 = Zl + g;
+        E2 = MSA_NEG;
+        Fo2 = MSA_NEG;
+      }
       int pubv = 0, consv = 0;
       unsigned spins = 0;
       fl_v4i ZA[4], FA[4], ZB[4], FB[4];
@@ -840,13 +850,15 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
         }
         if (q % FL_PS == 0) {  // pass 2 restarts here: each lane's (Z left, E~, F~, diagonal Z)
           if constexpr (R == 2) {  // rows 1 and 2: H~, R~, diagonal H~ / H~, R~, D~ (pass 2: unshifted)
+            // (affine: Z left, E~, diagonal Z / Z left, E~, F~)
+            constexpr int SH = GOT ? 1 : 0;
             unsigned long long* sp = a.snap + ((size_t)k * a.nseg + q / FL_PS) * 384 + lane;
             gstore(sp, ((unsigned long long)ep << 32) | (unsigned)Zl);
-            gstore(sp + 64, ((unsigned long long)ep << 32) | (unsigned)(E - 4 * oe));
+            gstore(sp + 64, ((unsigned long long)ep << 32) | (unsigned)(E - SH * 4 * oe));
             gstore(sp + 128, ((unsigned long long)ep << 32) | (unsigned)U);
             gstore(sp + 192, ((unsigned long long)ep << 32) | (unsigned)Zl2);
-            gstore(sp + 256, ((unsigned long long)ep << 32) | (unsigned)(E2 - 4 * oe));
-            gstore(sp + 320, ((unsigned long long)ep << 32) | (unsigned)(Fo2 - 4 * oe));
+            gstore(sp + 256, ((unsigned long long)ep << 32) | (unsigned)(E2 - SH * 4 * oe));
+            gstore(sp + 320, ((unsigned long long)ep << 32) | (unsigned)(Fo2 - SH * 4 * oe));
           } else {
             unsigned long long* sp = a.snap + ((size_t)k * a.nseg + q / FL_PS) * 256 + lane;
             gstore(sp, ((unsigned long long)ep << 32) | (unsigned)Zl);
@@ -941,6 +953,32 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
               Fo = dd;
               xz[kx] = h;
               xf[kx] = dd;
+            } else if constexpr (R == 2) {
+              // affine, two rows: row 1 takes the cell above from the previous lane's row 2, row 2
+              // from row 1 (Z and F~ at the same column), its diagonal from row 1's previous Z
+              const int upZ = dpp_shr1(Z[kx >> 2][kx & 3], Zl2);
+              const int upF = dpp_shr1(F[kx >> 2][kx & 3], Fo2);
+              const int sb = ((int)(s4b << (24 - 8 * kk))) >> 24;
+              const int flr1 = flb + g * (16 * q + kx);
+              const int e1 = imax(E, Zl);
+              const int f1 = imax(upF, upZ);
+              const int d1 = (FLOOR || HEAD) ? imax(U + sc, flr1) : U + sc;
+              int h1 = imax3(d1, e1, f1);
+              asm("" : "+v"(h1));
+              const int zprev = Zl;
+              U = upZ;
+              E = e1;
+              Zl = h1 - oe;
+              const int e2 = imax(E2, Zl2);
+              const int f2 = imax(f1, Zl);
+              const int d2 = (FLOOR || HEAD) ? imax(zprev + sb, flr1 + g) : zprev + sb;
+              int h2 = imax3(d2, e2, f2);
+              asm("" : "+v"(h2));
+              E2 = e2;
+              Fo2 = f2;
+              Zl2 = h2 - oe;
+              xz[kx] = Zl2;
+              xf[kx] = f2;
             } else {
               const int upZ = dpp_shr1(Z[kx >> 2][kx & 3], Zl);
               const int upF = dpp_shr1(F[kx >> 2][kx & 3], Fo);
@@ -1645,6 +1683,155 @@ __device__ __attribute__((noinline)) void fill_block_aff(kargs_c* ka, int blk, i
   if (lane == 0) a.blk[blk] = make_int4(bb, bi, bj, 0);
 }
 
+// Pass 2, affine, two rows per lane (R = 2: 128-row stripes, lane r holds rows 128s+2r+1 and
+// 128s+2r+2 at column cs + t - r): as fill_block_aff, both rows per step -- row 1 takes the cell
+// above (Z, F~) from the previous lane's row 2 (lane 0: the stripe above's bottom row), row 2 from
+// row 1 at the same column and its diagonal from row 1's previous Z.  A phase's bytes go out as
+// one 2 KiB block (row-1 segments, then row-2 segments: traceback_kernel<TB_SW, 2>'s layout).
+__device__ __attribute__((noinline)) void fill_block_aff2(kargs_c* ka, int blk, int lane, lds_int* lds) {
+  const FillArgs a = fill_args_of(ka);
+  const unsigned ep = a.ep;
+  const int m = a.m, n = a.n, S = (m + 127) / 128, g = a.g, oe = a.oe;
+  const int s = blk / a.nseg, seg = blk - s * a.nseg;
+  int bb = INT32_MIN, bi = 0, bj = 0;
+  if (s < S) {
+    const int P = fl_P(s, m, n, 2);
+    const int q0 = seg * FL_PS;
+    if (q0 < P) {
+      int q1 = min(P, q0 + FL_PS);
+      const int cs = fl_cs(s);
+      const int row_i = 128 * s + 2 * lane + 1;
+      const unsigned ac = (row_i <= m) ? (a.A[a.a_off + row_i - 1] & 7u) : 0u;
+      const unsigned ac2 = (row_i + 1 <= m) ? (a.A[a.a_off + row_i] & 7u) : 0u;
+      unsigned plo, phi, plo2, phi2;
+      fl_profile_aff(a.match, a.mismatch, g, oe, ac, plo, phi);
+      fl_profile_aff(a.match, a.mismatch, g, oe, ac2, plo2, phi2);
+      const int Bin = (s == 0) ? P - 1 : min(P - 1, fl_bmax(s, m, n, 2));
+      const unsigned long long* sp = a.snap + ((size_t)s * a.nseg + seg) * 384 + lane;
+      const unsigned long long* brz = a.br + (size_t)(s > 0 ? s - 1 : 0) * a.brw;
+      const unsigned long long* brf = a.br + (size_t)(S + (s > 0 ? s - 1 : 0)) * a.brw;
+      const int qb = (s > 0) ? min(q1, Bin + 1) : q0;
+      const int nv = 16 * max(0, qb - q0);
+      int Zl = 0, E = 0, U = 0, Zl2 = 0, E2 = 0, Fo2 = 0;
+      bool ready = (nv == 0);
+      for (int t2 = 0; !ready && t2 < (int)(FL_SPIN_MAX >> 2); ++t2) {
+        const unsigned long long gz = gload(brz + 16 * q0 + nv - 1), gf = gload(brf + 16 * q0 + nv - 1);
+        ready = __ballot((unsigned)(gz >> 32) != ep || (unsigned)(gf >> 32) != ep) == 0;
+        if (!ready) __builtin_amdgcn_s_sleep(FL_FSLEEP);
+      }
+      if (ready) {
+        ready = false;
+        for (int tries = 0; !ready && tries < (int)FL_SPIN_MAX; ++tries) {
+          const unsigned long long x0 = gload(sp), x1 = gload(sp + 64), x2 = gload(sp + 128), x3 = gload(sp + 192),
+                                   x4 = gload(sp + 256), x5 = gload(sp + 320);
+          bool ok = ((unsigned)(x0 >> 32) == ep) && ((unsigned)(x1 >> 32) == ep) && ((unsigned)(x2 >> 32) == ep) &&
+                    ((unsigned)(x3 >> 32) == ep) && ((unsigned)(x4 >> 32) == ep) && ((unsigned)(x5 >> 32) == ep);
+          Zl = (int)(unsigned)x0;
+          E = (int)(unsigned)x1;
+          U = (int)(unsigned)x2;
+          Zl2 = (int)(unsigned)x3;
+          E2 = (int)(unsigned)x4;
+          Fo2 = (int)(unsigned)x5;
+          for (int v = lane; v < nv; v += 64) {
+            const unsigned long long gz = gload(brz + 16 * q0 + v), gf = gload(brf + 16 * q0 + v);
+            ok = ok && ((unsigned)(gz >> 32) == ep) && ((unsigned)(gf >> 32) == ep);
+            *L(lds + v) = (int)(unsigned)gz;
+            *L(lds + 256 + v) = (int)(unsigned)gf;
+          }
+          ready = __ballot(!ok) == 0;
+          if (!ready) __builtin_amdgcn_s_sleep(8);
+        }
+      }
+      if (!ready) {
+        if (lane == 0) atomicExch(a.err, 15);
+        q1 = q0;
+      }
+      // row 0 (stripe 0): Z = g col - oe (H = 0), F~ = -inf
+      p2_stage<2>(lds, s, nv, 16 * (q1 - q0), lane,
+                  [&](int v, int k) { return k == 0 ? g * (cs + 16 * q0 + v) - oe : MSA_NEG; }, a.cod + a.cod_off,
+                  a.cod_copy, cs, q0);
+      const int flb = g * (128 * s + 1 + cs + lane);  // e(i+j) of row 1 at step 0 (row 2: + g)
+      int best = INT32_MIN, bt = -1, best2 = INT32_MIN, bt2 = -1;
+      fl_v4u* dp = reinterpret_cast<fl_v4u*>(a.outDir + (size_t)a.out_off + (size_t)s * a.pmax * 2048) + lane;
+      for (int q = q0; q < q1; ++q) {
+        int INZ[16], INF[16];
+        {
+          const lds_int4* srz = reinterpret_cast<const lds_int4*>(L(lds + 16 * (q - q0)));
+          const lds_int4* srf = reinterpret_cast<const lds_int4*>(L(lds + 256 + 16 * (q - q0)));
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const fl_v4i vz = srz[u], vf = srf[u];
+            INZ[4 * u] = vz.x; INZ[4 * u + 1] = vz.y; INZ[4 * u + 2] = vz.z; INZ[4 * u + 3] = vz.w;
+            INF[4 * u] = vf.x; INF[4 * u + 1] = vf.y; INF[4 * u + 2] = vf.z; INF[4 * u + 3] = vf.w;
+          }
+        }
+        const fl_v4u c4 = p2_codes(lds, q - q0, lane);
+        const unsigned cw[4] = {c4.x, c4.y, c4.z, c4.w};
+        const int flq = flb + 16 * g * q;
+        unsigned dw1[4], dw2[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const unsigned s4 = __builtin_amdgcn_perm(phi, plo, cw[u]);
+          const unsigned s4b = __builtin_amdgcn_perm(phi2, plo2, cw[u]);
+          unsigned word1 = 0, word2 = 0;
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) {
+            const int kx = 4 * u + kk;
+            const int sc = ((int)(s4 << (24 - 8 * kk))) >> 24;
+            const int sb = ((int)(s4b << (24 - 8 * kk))) >> 24;
+            const int flr = flq + g * kx, flr2 = flr + g;
+            // row 1
+            const int upZ = dpp_shr1(INZ[kx], Zl2);
+            const int upF = dpp_shr1(INF[kx], Fo2);
+            const int e1 = imax(E, Zl);
+            const int f1 = imax(upF, upZ);
+            const int d1 = U + sc;
+            int h1 = imax3(imax(d1, flr), e1, f1);
+            asm("" : "+v"(h1));
+            const unsigned hs1 = (h1 == flr) ? 0u : (h1 == d1 ? 1u : (h1 == e1 ? 2u : 3u));
+            word1 |= (hs1 | ((e1 == Zl) ? 4u : 0u) | ((f1 == upZ) ? 8u : 0u)) << (8 * kk);
+            if (h1 - flr > best) { best = h1 - flr; bt = 16 * q + kx; }
+            const int zprev = Zl;
+            U = upZ;
+            E = e1;
+            Zl = h1 - oe;
+            // row 2: diagonal = row 1's previous Z, above = row 1's new cell
+            const int e2 = imax(E2, Zl2);
+            const int f2 = imax(f1, Zl);
+            const int d2 = zprev + sb;
+            int h2 = imax3(imax(d2, flr2), e2, f2);
+            asm("" : "+v"(h2));
+            const unsigned hs2 = (h2 == flr2) ? 0u : (h2 == d2 ? 1u : (h2 == e2 ? 2u : 3u));
+            word2 |= (hs2 | ((e2 == Zl2) ? 4u : 0u) | ((f2 == Zl) ? 8u : 0u)) << (8 * kk);
+            if (h2 - flr2 > best2) { best2 = h2 - flr2; bt2 = 16 * q + kx; }
+            E2 = e2;
+            Fo2 = f2;
+            Zl2 = h2 - oe;
+          }
+          dw1[u] = word1;
+          dw2[u] = word2;
+        }
+        __builtin_nontemporal_store(fl_v4u{dw1[0], dw1[1], dw1[2], dw1[3]}, dp + (size_t)q * 128);
+        __builtin_nontemporal_store(fl_v4u{dw2[0], dw2[1], dw2[2], dw2[3]}, dp + (size_t)q * 128 + 64);
+      }
+      bb = (row_i <= m) ? best : INT32_MIN;
+      bi = row_i;
+      bj = cs + bt - lane;
+      if (row_i + 1 <= m && best2 > bb) {  // ties keep the upper row
+        bb = best2;
+        bi = row_i + 1;
+        bj = cs + bt2 - lane;
+      }
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const int ob = __shfl_xor(bb, off), oi = __shfl_xor(bi, off), oj = __shfl_xor(bj, off);
+    if (ob > bb || (ob == bb && (oi < bi || (oi == bi && oj < bj)))) { bb = ob; bi = oi; bj = oj; }
+  }
+  if (lane == 0) a.blk[blk] = make_int4(bb, bi, bj, 0);
+}
+
 // Pass 2, Gotoh (the reference's main_alignment_function path): block (stripe s, segment
 // seg) recomputes its FL_PS phases from SNAP (H~, R~, D~, diagonal H~ per lane) and the
 // stripe above's bottom row (H~ and D~ granules) and writes the tag bytes (T1's, T2's, T3's
@@ -1988,7 +2175,10 @@ __device__ __attribute__((noinline)) void fill_block_got2(kargs_c* ka, int blk, 
 // every input is complete when the blocks start, and the pass-2 code alone sets the register
 // budget: several waves per SIMD hide each other's LDS and store latency.
 template <bool FLOOR, bool TRACKPOS, int R, int FK>
-__global__ __launch_bounds__(FL_FILLW * 64) void flow_fill_kernel(KArgs a) {
+#ifndef FL_FILL_WPE
+#define FL_FILL_WPE 4  // waves per SIMD the pass-2 launch is sized for
+#endif
+__global__ __launch_bounds__(FL_FILLW * 64) __attribute__((amdgpu_waves_per_eu(FL_FILL_WPE, 8))) void flow_fill_kernel(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) int smem[];
   const int lane = threadIdx.x & 63;
   const int w = uni(threadIdx.x >> 6);
@@ -2001,6 +2191,7 @@ __global__ __launch_bounds__(FL_FILLW * 64) void flow_fill_kernel(KArgs a) {
     if (t >= a.nblk) break;
     if constexpr (FK == 2 && R == 2) fill_block_got2(ka, a.border[t], lane, wl);
     else if constexpr (FK == 2) fill_block_got(ka, a.border[t], lane, wl);
+    else if constexpr (FK == 1 && R == 2) fill_block_aff2(ka, a.border[t], lane, wl);
     else if constexpr (FK == 1) fill_block_aff(ka, a.border[t], lane, wl);
     else fill_block<FLOOR, TRACKPOS, R>(ka, a.border[t], lane, wl);
   }

@@ -1,4 +1,4 @@
-# quick GPU check: selected tests (K=pytest -k expr), then bench lines (BENCHES="name:args;...")
+# quick GPU check: selected tests (K=pytest -k expr), then bench lines (BENCHES="name:[VAR=val ...] args;...")
 set -o pipefail
 mkdir -p gpurun_out
 if [ -n "$K" ]; then
@@ -8,7 +8,9 @@ fi
 IFS=';' read -ra BL <<< "$BENCHES"
 for b in "${BL[@]}"; do
   name="${b%%:*}"; args="${b#*:}"
-  timeout -k 10 300 python -u bench.py --no-cpu-baseline $args > gpurun_out/bq_$name.json 2> gpurun_out/bq_$name.err || { echo "bench $name failed"; tail -20 gpurun_out/bq_$name.err; exit 1; }
+  pre=""; rest=""
+  for tok in $args; do if [ -z "$rest" ] && [[ "$tok" == *=* ]] && [[ "$tok" != --* ]]; then pre="$pre $tok"; else rest="$rest $tok"; fi; done
+  timeout -k 10 300 env $pre python -u bench.py --no-cpu-baseline $rest > gpurun_out/bq_$name.json 2> gpurun_out/bq_$name.err || { echo "bench $name failed"; tail -20 gpurun_out/bq_$name.err; exit 1; }
   python - "$name" <<'PY'
 import json, sys
 n = sys.argv[1]

@@ -562,6 +562,32 @@ def test_c3_full_size(oracle, dev, LB):
     assert info["mode"] == "chunked" and info["converged"] == 1 and info["chunks"] >= 4, info
 
 
+@pytest.mark.parametrize("which", ["synthetic", "dissimilar"])
+def test_c3_other_inputs(oracle, dev, LB, which):
+    """C3 beyond the bench's real pair: SURVEY §8(d)'s synthetic input (100,000 i.i.d. ACGT, B = A mutated 1% /
+    0.1%, seed 0x5EED0003 -- converges in every chunk) and a dissimilar real pair (ABCB1 x KIT, 81,835 each --
+    rank convergence fails, the exact launch behind the chunks recomputes it): score and the digest of every
+    in-band H cell equal the banded oracle's."""
+    import torch
+    from cse305_parallel_sequence_alignment_amd import data
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+
+    if which == "synthetic":
+        A, B = data.c3_pair(synthetic=True)
+    else:
+        A, B = data.bundled()[0][:81835], data.bundled()[15][:81835]
+    pl = Plan(LB.NW_BANDED, LB.CELLS_H, [len(A)], [len(B)], [0], [0], match=1, mismatch=0, gap_open=3,
+              gap_extend=1, band=512)
+    H = torch.empty(pl.cells_elems, dtype=torch.int32, device=dev)
+    pl.run(_dev(A, dev), _dev(B, dev), H)
+    score, digest = oracle.banded_ref(A, B, 512, 1.0, 2.0, want_digest=True)
+    assert pl.results()[0]["score"] == int(score)
+    assert pl.checksum(H) == digest
+    info = pl.run_info()
+    assert info["mode"] == "chunked" and info["converged"] == (1 if which == "synthetic" else 0), info
+    assert pl.error() == 0
+
+
 def _similar(rng, m, sub=0.02, indel=0.002):
     """A random A and B = A with substitutions and short indels (length ~m)."""
     A = rs(rng, m)
@@ -679,9 +705,10 @@ def test_sw_affine_flow_dir_bytes(dev, LB, m, n, scoring):
         pl.run(_dev(A, dev), _dev(B, dev), D)
         r = pl.results()[0]
         info = pl.run_info()
-        out.append((pl.deskew_dir(D.cpu().numpy(), 0, pl.stripe_meta()), r["score"], tuple(r["end"]), info["mode"]))
-    (d1, s1, e1, mode1), (d0, s0, e0, _) = out
-    assert mode1 == "flow"
+        out.append((pl.deskew_dir(D.cpu().numpy(), 0, pl.stripe_meta()), r["score"], tuple(r["end"]), info["mode"],
+                    pl.geom[0].rows_per_lane))
+    (d1, s1, e1, mode1, r1), (d0, s0, e0, _, _) = out
+    assert mode1 == "flow" and r1 == 2  # the flow kernel's two-rows-per-lane layout
     assert (s1, e1) == (s0, e0)
     assert np.array_equal(d1[1:, 1:], d0[1:, 1:])
 
