@@ -22,6 +22,7 @@
 #include "../../include/msa.h"
 #include "msa_kernels.hip"
 #include "msa_flow.hip"
+#include "msa_band.hip"
 #include "msa_rowsweep.hip"
 #include "msa_traceback.hip"
 
@@ -366,6 +367,8 @@ struct msa_plan {
   int grid = 1;
   int threads = 64;
   bool flow = false;   // flow_kernel (single-pair SW linear) instead of stripe_kernel
+  bool band_k = false;  // band_kernel (banded single pair, msa_band.hip)
+  int band_items = 0;   // band_kernel: items of the larger of its launches (granule slots)
   bool flow2 = false;  // + pass-2 blocks inside the same launch (O_H)
   kfn_t fill_fn = nullptr;  // long pairs: pass 2 as a launch of its own behind pass 1
   int fill_grid = 0;
@@ -551,8 +554,11 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   // reference-Gotoh (start type -1, tagged) pair with direction bytes (two values per link
   // column, 4 code rings); the column codes stream through fixed-size LDS rings, so any n fits
   const bool aff = kalg == MSA_ALG_SWA || kalg == MSA_ALG_REF1;
-  const size_t flow_lds = (size_t)(FL_FLAGS + (FL_W + 1) * 256 * (aff ? 2 : 1)) * 4 +
-                          (size_t)(aff ? 4 : FL_NCOPY) * FL_CSTR + ((aff || FL_HO != 2) ? 0 : FL_SINK);
+  // the code copies: whole rows when they fit (kp.code_whole: no ring bookkeeping), else rings
+  const size_t flow_lds0 = (size_t)(FL_FLAGS + (FL_W + 1) * 256 * (aff ? 2 : 1)) * 4 + ((aff || FL_HO < 2) ? 0 : FL_SINK);
+  const size_t flow_whole = flow_lds0 + (size_t)(aff ? 4 : FL_NCOPY) * (fl_code_bytes((int)desc->n[0]) + 16);
+  const bool code_whole = flow_whole <= 96 * 1024;
+  const size_t flow_lds = code_whole ? flow_whole : flow_lds0 + (size_t)(aff ? 4 : FL_NCOPY) * FL_CSTR;
   // affine: profile bytes score + 2e + (o - e) must be int8
   const bool aff_ok = kalg == MSA_ALG_SWA && out_mode == MSA_OUT_DIR && desc->gap_extend >= 0 &&
                       desc->gap_open >= desc->gap_extend &&
@@ -601,6 +607,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   kp.h = desc->gap_open - desc->gap_extend;
   kp.start_type = desc->start_type;
   kp.band = band;
+  kp.code_whole = (flow && code_whole) ? 1 : 0;
   kp.single = single ? 1 : 0;
   kp.n_pairs = (int)desc->n_pairs;
   if (kalg == MSA_ALG_NWA && kp.h < 0) { delete P; return MSA_ERR_UNSUPPORTED; }
@@ -800,7 +807,72 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
 #define MSA_CHUNK_MIN 10   // stripes per chunk, at least
 #endif
   constexpr int kWarm = MSA_CHUNK_WARM;
+  // Banded single pair (C3-type): band_kernel (msa_band.hip), flag-synchronised chains of 4-stripe
+  // items.  The exact launch chains all of the pair's items; chunked (rank convergence, >= 4
+  // chunks) runs chunks of C output stripes, each started W stripes early from a guessed row, with
+  // the exact launch queued behind as the fallback.  MSA_BAND_WARM / MSA_BAND_CHUNK (diagnostic)
+  // override the warm-up and chunk stripes (multiples of 4).
   if (single && kalg == MSA_ALG_NWA && band >= 0 && (out_mode == MSA_OUT_H || out_mode == MSA_OUT_NONE)) {
+    const int m0 = (int)desc->m[0], n0 = (int)desc->n[0];
+    const int S = (m0 + 63) / 64;
+    const int L8 = bk_code_bytes(m0, n0, band);
+    const size_t blds = bk_lds_bytes(L8);
+    const int bocc = (blds <= 160 * 1024) ? kernel_shape(band_kernel, (BK_W + 1) * 64, blds) : -1;
+    if (bocc > 0) {
+      auto env_int = [](const char* name, int dflt) {
+        const char* e = std::getenv(name);
+        return e ? std::atoi(e) : dflt;
+      };
+      const int warm = std::max(0, env_int("MSA_BAND_WARM", kWarm) / BK_W * BK_W);
+      const int cc = std::max(BK_W, env_int("MSA_BAND_CHUNK", 12) / BK_W * BK_W);
+      const int nch = (S + cc - 1) / cc;
+      msa_kparams ek = kp;  // the exact launch
+      ek.single = 1;
+      ek.groups = (S + BK_W - 1) / BK_W;
+      ek.n_items = ek.groups;
+      ek.chunk_c = S;
+      ek.chunk_warm = 0;
+      ek.lds_code_bytes = L8;
+      ek.sched_cap = 0;
+      P->band_k = true;
+      P->fn = band_kernel;
+      P->W = BK_W;
+      P->KS = 16;
+      P->threads = (BK_W + 1) * 64;
+      P->lds_bytes = blds;
+      P->grid = std::max(1, std::min(ek.n_items, ncu * bocc));
+      kp = ek;
+      P->band_items = ek.n_items;
+      if (nch >= 4 && out_mode == MSA_OUT_H) {
+        P->chunked = true;
+        P->n_chunks = nch;
+        P->fb_kp = ek;
+        P->fb_fn = band_kernel;
+        P->fb_grid = P->grid;
+        P->fb_threads = P->threads;
+        P->fb_lds = blds;
+        kp.single = 2;
+        kp.chunk_c = cc;
+        kp.chunk_warm = warm;
+        // item slots per chunk: its warm-up + output stripes in items of BK_W (a chunk whose warm-up
+        // would reach the matrix border starts at row 0 instead -- band_kernel -- and so has more)
+        int ipc = 1;
+        for (int c2 = 0; c2 < nch; ++c2) {
+          const int ks0 = c2 * cc, ke = std::min(S, ks0 + cc);
+          int kb = ks0 - warm;
+          if (kb < 0 || kb * 64 <= band + 64) kb = 0;
+          ipc = std::max(ipc, (ke - kb + BK_W - 1) / BK_W);
+        }
+        kp.groups = ipc;
+        kp.n_items = nch * kp.groups;
+        P->grid = std::max(1, std::min(kp.n_items, ncu * bocc));
+        P->band_items = std::max(P->band_items, kp.n_items);
+        P->ckw = (2 * band + 1 + 3) & ~3;
+      }
+    }
+  }
+  if (single && kalg == MSA_ALG_NWA && band >= 0 && (out_mode == MSA_OUT_H || out_mode == MSA_OUT_NONE) &&
+      !P->band_k) {
     const int S = (int)((desc->m[0] + 63) / 64);
     const int cc = std::max(MSA_CHUNK_MIN, (S + ncu - 1) / ncu);
     const int nch = (S + cc - 1) / cc;
@@ -854,7 +926,13 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   if (!P->alloc(&P->d_res, sizeof(PairResult) * desc->n_pairs)) return fail();
   if (!P->alloc(&P->d_sum, 64)) return fail();
   const int single_items = P->chunked ? P->fb_kp.n_items : kp.n_items;  // single-mode launch's items
-  if ((single || kp.single == 3) && single_items > 1) {
+  if (P->band_k && P->band_items > 1) {
+    // band_kernel: item t publishes (Z, F~) of its last row into slot t (chunked and exact launches)
+    P->gbuf_stride = (int)(((desc->n[0] + 2 * MSA_GOFF + 16) + 15) & ~15);
+    const size_t gb = (size_t)P->band_items * 2 * P->gbuf_stride * sizeof(unsigned long long);
+    if (!P->alloc(&P->d_gbuf, gb)) return fail();
+    if (hipMemset(P->d_gbuf, 0, gb) != hipSuccess) return fail();
+  } else if ((single || kp.single == 3) && single_items > 1) {
     int64_t nmax = 0;
     for (int64_t p = 0; p < desc->n_pairs; ++p) nmax = std::max(nmax, desc->n[p]);
     P->gbuf_stride = (int)(((nmax + 2 * MSA_GOFF + 16) + 15) & ~15);
@@ -1007,7 +1085,11 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
     HIPCHK(hipGetLastError());
     KArgs b = a;
     b.kp = P->fb_kp;
-    b.kp.epoch = ep;
+    // its own epoch: the band kernel's chunked launch leaves granules of this run's epoch in the
+    // slots the exact launch reads
+    uint32_t ep2 = g_epoch.fetch_add(1) + 1;
+    if (ep2 == 0) ep2 = g_epoch.fetch_add(1) + 1;
+    b.kp.epoch = ep2;
     b.ck = nullptr;
     b.skip = P->d_skip;
     hipLaunchKernelGGL(P->fb_fn, dim3(P->fb_grid), dim3(P->fb_threads), P->fb_lds, st, b);

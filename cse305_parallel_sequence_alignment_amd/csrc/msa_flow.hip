@@ -55,6 +55,9 @@ namespace msa {
 // n <= ~19.5k and affine / Gotoh at ~37k).
 #define FL_CRING 4096
 #define FL_CSTR (FL_CRING + 16)
+// When a copy's whole code row fits the LDS budget (kp.code_whole, msa_capi.hip), the copies are
+// linear (stride L8 + 16, no wrap) and io-in never holds blocks back for ring space: the ring's
+// refill bookkeeping measured +6 us on C2 (10k, 0.459 -> 0.465 ms).
 #ifndef FL_PS
 #define FL_PS 8         // phases per pass-2 segment (pass 1 saves its state every FL_PS phases)
 #endif
@@ -73,7 +76,9 @@ namespace msa {
 #ifndef FL_HO
 #define FL_HO 0         // SW-linear hand-off: 0 = 16 ds_write_addtid_b32, 1 = 8 ds_write_b64 (both lane 63
                         // alone), 2 = 4 ds_write_b128 of every lane (lanes 0..62 into a sink; measured
-                        // C2 0.478 vs 0.455 ms: the 1 KiB writes cost more LDS time than the exec switch)
+                        // C2 0.478 vs 0.455 ms: the 1 KiB writes cost more LDS time than the exec switch),
+                        // 3 = a DPP shift register (one wave_shl:1 per step collects lane 63's values in
+                        // lanes 48..63) and two every-lane ds_write_b32 (lanes 0..47 into the sink)
 #endif
 #ifndef FL_IOSLEEP
 #define FL_IOSLEEP 1    // s_sleep of an idle io wave
@@ -224,6 +229,16 @@ __device__ __forceinline__ void ds_handoff_all(unsigned wa, const fl_v4i (&x)[4]
       :
       : [a] "v"(wa), [x0] "v"(x[0]), [x1] "v"(x[1]), [x2] "v"(x[2]), [x3] "v"(x[3]), [pa] "v"(pa), [pv] "v"(pv)
       : "memory");
+}
+
+// FL_HO 3: lanes 48..63 hold lane 63's 16 values of the phase (the shift register); every lane
+// writes one dword -- lanes 48..63 to the ring block, the others to the sink -- then the counter
+// (lane 63 to its flag, the others to the sink).  2 DS ops, no exec switch, no wait states.
+__device__ __forceinline__ void ds_handoff_sh(unsigned wa, int x, unsigned pa, int pv) {
+  asm volatile("ds_write_b32 %[a], %[x]\n\tds_write_b32 %[pa], %[pv]"
+               :
+               : [a] "v"(wa), [x] "v"(x), [pa] "v"(pa), [pv] "v"(pv)
+               : "memory");
 }
 
 // Affine hand-off: lane 63 alone writes its 16 Z and 16 F~ of the phase as 8 b128 writes
@@ -379,6 +394,13 @@ struct FillArgs {
 // setup and every access a private-memory load).
 typedef const __attribute__((address_space(4))) struct KArgs kargs_c;
 __device__ __forceinline__ FillArgs fill_args_of(kargs_c* k) {
+#ifdef FL_KA_UNI
+  // (measured: the pointer made wave-uniform -- scalar loads of the arguments instead of vector
+  // loads -- made C2 slower, 0.466 -> 0.476 ms; off)
+  const unsigned long long kv = (unsigned long long)k;
+  k = (kargs_c*)(((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(kv >> 32)) << 32) |
+                 (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)kv));
+#endif
   const msa_pair_desc pd = k->pairs[0];
   return FillArgs{k->A, k->cod, k->br, k->snap, k->outH, k->blk, k->err, k->cod_copy, pd.a_off, pd.cod_off,
                   pd.out_off, pd.m, pd.n, pd.pmax, k->nseg, k->brw, k->kp.match, k->kp.mismatch, k->kp.gap_ext,
@@ -389,7 +411,16 @@ __device__ __forceinline__ FillArgs fill_args_of(kargs_c* k) {
   };
 }
 template <bool FLOOR, bool TRACKPOS, int R>
+#ifndef FL_FB_PTR
+#define FL_FB_VAL  // SW-linear pass-2 blocks take their arguments by value (C2 0.4646 -> 0.4604 ms against the kernarg pointer)
+#endif
+#ifdef FL_FB_VAL
+__device__ __attribute__((noinline)) void fill_block(const FillArgs fa, int blk, int lane, lds_int* lds);
+#define FL_FB_ARG(ka_) fill_args_of(ka_)
+#else
 __device__ __attribute__((noinline)) void fill_block(kargs_c* ka, int blk, int lane, lds_int* lds);
+#define FL_FB_ARG(ka_) (ka_)
+#endif
 __device__ __attribute__((noinline)) void fill_block_aff(kargs_c* ka, int blk, int lane, lds_int* lds);
 __device__ __attribute__((noinline)) void fill_block_aff2(kargs_c* ka, int blk, int lane, lds_int* lds);
 __device__ __attribute__((noinline)) void fill_block_got(kargs_c* ka, int blk, int lane, lds_int* lds);
@@ -417,8 +448,11 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
   // taken); dummy sink 96..127
   int* flags = smem;
   int* rings = smem + FL_FLAGS;                                               // [W+1 links][NV][256]
-  uint8_t* codes = reinterpret_cast<uint8_t*>(rings + (W + 1) * 256 * NV);  // [NCP][FL_CSTR] rings
+  uint8_t* codes = reinterpret_cast<uint8_t*>(rings + (W + 1) * 256 * NV);  // [NCP][cstr] rings / rows
   const int L8 = kp.lds_code_bytes;  // bytes of a copy's whole (linear) code row
+  const bool cwhole = kp.code_whole != 0;
+  const int cstr = cwhole ? L8 + 16 : FL_CSTR;               // bytes per LDS copy
+  const unsigned cmask = cwhole ? 0xffffffffu : (unsigned)(FL_CRING - 1);
   const msa_pair_desc pd = a.pairs[0];
   const int m = pd.m, n = pd.n;
   const int S = (m + 64 * R - 1) / (64 * R);
@@ -473,7 +507,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
         else if constexpr (GOT) fill_block_got(ka, a.border[t], lane, wl);
         else if constexpr (AFF && R == 2) fill_block_aff2(ka, a.border[t], lane, wl);
         else if constexpr (AFF) fill_block_aff(ka, a.border[t], lane, wl);
-        else fill_block<FLOOR, TRACKPOS, R>(ka, a.border[t], lane, wl);
+        else fill_block<FLOOR, TRACKPOS, R>(FL_FB_ARG(ka), a.border[t], lane, wl);
       }
 #ifdef MSA_STAMPS
       wg_stamp(1, __builtin_amdgcn_s_memrealtime());
@@ -533,6 +567,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
       // 63 + FL_OFF - 7 + 16 c >= 16 c + 10, and loading chunk y overwrites chunk y - FL_CRING
       // (and, at ring position 0, the guard that mirrors it).
       auto code_cap = [&]() __attribute__((always_inline)) {
+        if (cwhole) return 1 << 30;
         int c = 1 << 30;
 #pragma unroll
         for (int w2 = 0; w2 < W; ++w2)
@@ -557,11 +592,11 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
           for (int r = 0; r < 4; ++r) {
             const int c = c0 + r * 64 + lane;
             const int x = c & (NCP - 1), y = Yr + 16 * (c / NCP);
-            const int pos = y & (FL_CRING - 1);
+            const int pos = (int)((unsigned)y & cmask);
             const fl_v4i d{v[r].x, v[r].y, v[r].z, v[r].w};
             if (c < tot) {
-              *(lds_int4*)(codes + x * FL_CSTR + pos) = d;
-              if (pos == 0) *(lds_int4*)(codes + x * FL_CSTR + FL_CRING) = d;  // the guard
+              *(lds_int4*)(codes + x * cstr + pos) = d;
+              if (!cwhole && pos == 0) *(lds_int4*)(codes + x * cstr + FL_CRING) = d;  // the guard
             }
           }
         }
@@ -737,7 +772,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
       {
         const int c0 = cs - lane + FL_OFF;
         const int x = c0 & (NCP - 1);
-        a_cring = lds_addr(reinterpret_cast<int*>(codes + x * FL_CSTR));
+        a_cring = lds_addr(reinterpret_cast<int*>(codes + x * cstr));
         y_code = (unsigned)(c0 - x);
       }
       // step 0: lane r at column cs - r (virtual, H = 0): its left cell's Z, the diagonal Z
@@ -781,7 +816,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
         F[1] = ds_read_b128<1040>(ra);
         F[2] = ds_read_b128<1056>(ra);
         F[3] = ds_read_b128<1072>(ra);
-        ds_read_codes16(a_cring + ((y_code + 16u * (unsigned)q) & (FL_CRING - 1)), Cl, Ch);
+        ds_read_codes16(a_cring + ((y_code + 16u * (unsigned)q) & cmask), Cl, Ch);
       };
       auto wait_flag = [&](unsigned addr, int& val, int need) __attribute__((always_inline)) {
         while (val < need) {
@@ -1093,8 +1128,15 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
 #if FL_HO == 2
       // every-lane hand-off: lanes 0..62 (and lane 63 with nothing to hand off) write to the
       // sink after the code copies (FL_SINK bytes, shared by the compute waves, never read)
-      const unsigned a_sink = lds_addr(codes + FL_NCOPY * FL_CSTR) + 16u * (unsigned)lane;
-      const unsigned a_pa = (lane == 63) ? a_prog_me : lds_addr(codes + FL_NCOPY * FL_CSTR) + 4u * (unsigned)lane;
+      const unsigned a_sink = lds_addr(codes + FL_NCOPY * cstr) + 16u * (unsigned)lane;
+      const unsigned a_pa = (lane == 63) ? a_prog_me : lds_addr(codes + FL_NCOPY * cstr) + 4u * (unsigned)lane;
+#elif FL_HO == 3
+      // shift-register hand-off: lanes 48..63 write the ring block (wa + 4 (lane - 48)), the others the
+      // sink after the code copies (shared by the compute waves, never read); the counter likewise
+      const unsigned a_sink = lds_addr(codes + FL_NCOPY * cstr) + 4u * (unsigned)lane;
+      const unsigned a_pa = (lane == 63) ? a_prog_me : a_sink + 256u;
+      const bool sh_lane = lane >= 48;
+      int shreg = 0;
 #endif
       unsigned plo, phi, plo2 = 0, phi2 = 0;
       fl_profile<GS, FLOOR>(kp.match, kp.mismatch, g, ac, plo, phi);
@@ -1105,7 +1147,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
       {
         const int c0 = cs - lane + FL_OFF;
         const int x = c0 & (FL_NCOPY - 1);
-        a_cring = lds_addr(reinterpret_cast<int*>(codes + x * FL_CSTR));
+        a_cring = lds_addr(reinterpret_cast<int*>(codes + x * cstr));
         y_code = (unsigned)(c0 - x);
       }
       // G-space: H = G - g(i+j), i+j = 64k + 1 + cs + t for every lane of step t
@@ -1138,7 +1180,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
         IN[1] = ds_read_b128<16>(ra);
         IN[2] = ds_read_b128<32>(ra);
         IN[3] = ds_read_b128<48>(ra);
-        CW = ds_read2_b64(a_cring + ((y_code + 16u * (unsigned)q) & (FL_CRING - 1)));
+        CW = ds_read2_b64(a_cring + ((y_code + 16u * (unsigned)q) & cmask));
       };
       auto reread_in = [&](int q, fl_v4i (&IN)[4]) __attribute__((always_inline)) {
         ds_reread_b128x4(a_ring_in + (unsigned)((q & (FL_RINGB - 1)) * 64), IN);
@@ -1232,9 +1274,14 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
 #if FL_HO == 2
         fl_v4i xo4[4];
 #define FL_XO(kx_) xo4[(kx_) >> 2][(kx_) & 3]
+#elif FL_HO == 3
+#define FL_PUT(kx_, v_) (shreg = dpp_shl1((v_), shreg))
 #else
         int xo[16];
 #define FL_XO(kx_) xo[kx_]
+#endif
+#ifndef FL_PUT
+#define FL_PUT(kx_, v_) (FL_XO(kx_) = (v_))
 #endif
         int pubn = 0;
         const int negct = negct0 - 16 * g * q;
@@ -1249,7 +1296,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
             const int s = ((int)(s4 << (24 - 8 * kk))) >> 24;
             if constexpr (R == 1) {
               const int h = fl_step<GS, FLOOR>(IN[kx >> 2][kx & 3], s, X, U, g);
-              FL_XO(kx) = X;
+              FL_PUT(kx, X);
               if constexpr (BEST) hv[kx] = GS ? h + negct + gk[kx] : h;
             } else {
               // row 1's up = the previous lane's row 2 (lane 0: the producer's value);
@@ -1266,7 +1313,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
               if constexpr (FLOOR) h2 = imax(h2, 0);
               asm("" : "+v"(h2));
               X2 = GS ? h2 : h2 - g;
-              FL_XO(kx) = X2;
+              FL_PUT(kx, X2);
             }
           }
         }
@@ -1286,12 +1333,15 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
         const unsigned wa = wr ? a_ring_out + (unsigned)((bq & (FL_RINGB - 1)) * 64) : a_dummy;
 #if FL_HO == 2
         ds_handoff_all((lane == 63 && wr) ? wa : a_sink, xo4, a_pa, q + 1);
+#elif FL_HO == 3
+        ds_handoff_sh((sh_lane && wr) ? wa - 192u + 4u * (unsigned)lane : a_sink, shreg, a_pa, q + 1);
 #elif FL_HO == 1
         ds_handoff_b64(m63, wa, xo, a_prog_me, q + 1);
 #else
         ds_handoff_tid(m63, wa - 252u, xo, a_prog_me, q + 1);  // (-6.5% on C2 vs four single-lane b128 writes)
 #endif
 #undef FL_XO
+#undef FL_PUT
 #ifdef MSA_STAMPS
         if (q == dq) FL_STAMP(0, 3, __builtin_amdgcn_s_memrealtime());
 #endif
@@ -1401,8 +1451,12 @@ __device__ __forceinline__ fl_v4u p2_codes(lds_int* lds, int k, int lane) {
 // R = 2: lane r holds rows 128s+2r+1 (X/U) and 128s+2r+2 (X2); cells go to the
 // R = 2 layout (per 4 steps: the wave's row-1 int4s, then its row-2 int4s).
 template <bool FLOOR, bool TRACKPOS, int R>
+#ifdef FL_FB_VAL
+__device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, int lane, lds_int* lds) {
+#else
 __device__ __attribute__((noinline)) void fill_block(kargs_c* ka, int blk, int lane, lds_int* lds) {
   const FillArgs a = fill_args_of(ka);
+#endif
   constexpr bool GS = !FLOOR;
   const unsigned ep = a.ep;
   const int m = a.m, n = a.n, S = (m + 64 * R - 1) / (64 * R), g = a.g;
@@ -2193,7 +2247,7 @@ __global__ __launch_bounds__(FL_FILLW * 64) __attribute__((amdgpu_waves_per_eu(F
     else if constexpr (FK == 2) fill_block_got(ka, a.border[t], lane, wl);
     else if constexpr (FK == 1 && R == 2) fill_block_aff2(ka, a.border[t], lane, wl);
     else if constexpr (FK == 1) fill_block_aff(ka, a.border[t], lane, wl);
-    else fill_block<FLOOR, TRACKPOS, R>(ka, a.border[t], lane, wl);
+    else fill_block<FLOOR, TRACKPOS, R>(FL_FB_ARG(ka), a.border[t], lane, wl);
   }
 }
 

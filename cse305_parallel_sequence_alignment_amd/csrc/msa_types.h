@@ -77,6 +77,7 @@ typedef struct msa_kparams {
   int32_t groups;           // single == 3 (a batch too small to fill the chip): items per pair (or
                             //   per packed couple), each W consecutive stripes, chained through
                             //   granules like single mode; every pair has the same m
+  int32_t code_whole;       // flow kernels: 1 = every LDS code copy holds the whole row (no ring)
 } msa_kparams;
 
 #ifdef __cplusplus

@@ -18,7 +18,7 @@ from pathlib import Path
 src, wl, rnd = Path(sys.argv[1]), sys.argv[2], sys.argv[3]
 # the DP kernel of the workload: flow_kernel (single-pair SW linear, pass 1 + pass-2
 # blocks in one launch) or stripe_kernel (everything else)
-KERNELS = ("flow_kernel", "stripe_kernel")
+KERNELS = ("flow_kernel", "stripe_kernel", "band_kernel")
 dst = Path(__file__).resolve().parent.parent / "profiles"
 dst.mkdir(exist_ok=True)
 

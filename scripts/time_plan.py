@@ -16,14 +16,23 @@ from cse305_parallel_sequence_alignment_amd import _lib as LB, data
 from cse305_parallel_sequence_alignment_amd.plan import Plan
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--workload", default="ref", choices=["c2", "c5", "ref"])
+ap.add_argument("--workload", default="ref", choices=["c2", "c5", "ref", "c3", "c3d", "c3syn"])
 ap.add_argument("--ref-len", type=int, default=10000)
 ap.add_argument("--ref-pair", default="0,1")
 ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--check", action="store_true", help="c2: compare the H checksum with the oracle's")
 args = ap.parse_args()
 if args.workload == "c2":
     A, B = data.c2_pair(0)
     pl = Plan(LB.SW_LINEAR, LB.CELLS_H, [len(A)], [len(B)], [0], [0], match=1, mismatch=0, gap_open=1, gap_extend=1)
+    out = torch.empty(pl.cells_elems, dtype=torch.int32, device="cuda")
+elif args.workload.startswith("c3"):
+    if args.workload == "c3d":  # a dissimilar real pair (rank convergence fails: the exact launch runs)
+        A, B = data.bundled()[0][:81835], data.bundled()[15][:81835]
+    else:
+        A, B = data.c3_pair(synthetic=args.workload == "c3syn")
+    pl = Plan(LB.NW_BANDED, LB.CELLS_H, [len(A)], [len(B)], [0], [0], match=1, mismatch=0, gap_open=3,
+              gap_extend=1, band=512)
     out = torch.empty(pl.cells_elems, dtype=torch.int32, device="cuda")
 elif args.workload == "c5":
     A, B = data.c5_pair(0)
@@ -44,5 +53,18 @@ kms = []
 for _ in range(args.reps):
     pl.run(dA, dB, out)
     kms.append(pl.kernel_ms())
-print(json.dumps(dict(workload=args.workload, m=len(A), n=len(B), lib=str(LB.LIB_PATH.name), kernel_ms=kms,
-                      error=pl.error())), flush=True)
+res = dict(workload=args.workload, m=len(A), n=len(B), lib=str(LB.LIB_PATH.name), kernel_ms=kms, error=pl.error(),
+           median_ms=sorted(kms)[len(kms) // 2])
+if args.workload.startswith("c3"):
+    res["run_info"] = pl.run_info()
+if args.check and args.workload.startswith("c3"):
+    from oracle import oracle as O
+
+    score, digest = O.banded_ref(A, B, 512, 1.0, 2.0, want_digest=True)
+    res["h_ok"] = bool(pl.checksum(out) == digest and pl.results()[0]["score"] == int(score))
+if args.check and args.workload == "c2":
+    from oracle import oracle as O
+
+    o = O.sw(A, B, 1, 0, 1, 1, want_h=True)
+    res["h_ok"] = bool(pl.checksum(out) == O.checksum_h(o["H"]) and pl.results()[0]["score"] == o["score"])
+print(json.dumps(res), flush=True)
