@@ -482,7 +482,11 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
   // except that the first 8 arrivals take chunk = arrival: every chunk's first item is then
   // claimed by a running workgroup even if the workgroup with blockIdx c is not resident (CUs
   // held by other launches), and a chunk's later items wait only on claimed ones.
+#ifdef FL_GRP_BLK
+  const int grp = (int)(blockIdx.x & 7);  // (diagnostic: round 3's choice)
+#else
   const int grp = arrival < 8 ? arrival : (int)(blockIdx.x & 7);
+#endif
   if constexpr (SAVE) {
 #ifdef MSA_STAMPS
     if (a.stamps && threadIdx.x == 0 && blockIdx.x < 2048)
