@@ -60,7 +60,8 @@ OPS_PER_CELL = {"c4": 8.0, "c5": 12.0, "ref": 13.0}  # ref: T1 add + 2 max, T2 /
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks); default 1, or WORLD_SIZE when a launcher (torchrun) started this process")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c2", choices=["c2", "c4", "c3", "c5", "ref"])
@@ -133,32 +134,34 @@ def cpu_baseline(wl: str, A: bytes, B: bytes, cores: int, pairs=None):
                 points=pts)
 
 
-def load_wave_time(wl: str):
+def _pmc_profile(wl: str, shape: str):
+    """The newest committed PMC profile (profiles/<round>_<name>_pmc.json, scripts/pmc_summary.py) of THIS
+    workload and shape ("m,n", or "pairs=P" for a c4 rank's share): a profile of another size or another
+    rank share is never used for this run's line."""
+    for p in sorted((REPO / "profiles").glob("*_pmc.json"), reverse=True):
+        try:
+            d = json.loads(p.read_text())
+        except Exception:
+            continue
+        if d.get("workload", "").startswith(wl) and d.get("shape") == shape:
+            return p.name, d
+    return None, None
+
+
+def load_wave_time(wl: str, shape: str):
     """Where the DP kernel's waves spend their time (parked on s_waitcnt / barriers, issue-stalled,
-    issuing VALU / LDS / SALU; fractions of SQ_WAVE_CYCLES) from the newest committed PMC profile of
-    the workload (scripts/pmc_summary.py), or None."""
-    for p in sorted((REPO / "profiles").glob("*_pmc.json"), reverse=True):
-        try:
-            d = json.loads(p.read_text())
-        except Exception:
-            continue
-        if d.get("workload") == wl and d.get("wave_time"):
-            return dict(d["wave_time"], source=p.name)
-    return None
+    issuing VALU / LDS / SALU; fractions of SQ_WAVE_CYCLES), or None."""
+    name, d = _pmc_profile(wl, shape)
+    return dict(d["wave_time"], source=name) if d and d.get("wave_time") else None
 
 
-def load_traffic(wl: str):
-    """Per-launch HBM bytes of the DP kernel from the newest committed PMC profile
-    (profiles/<round>_<wl>_pmc.json, scripts/pmc_summary.py: 2 x FETCH_SIZE + WRITE_SIZE per the
-    MI355X guide's gfx950 correction), or None."""
-    for p in sorted((REPO / "profiles").glob("*_pmc.json"), reverse=True):
-        try:
-            d = json.loads(p.read_text())
-        except Exception:
-            continue
-        if d.get("workload") == wl and d.get("hbm_bytes_per_launch"):
-            return float(d["hbm_bytes_per_launch"]["total"])
-    return None
+def load_traffic(wl: str, shape: str):
+    """Per-launch HBM bytes of the DP kernel (2 x FETCH_SIZE + WRITE_SIZE per the MI355X guide's gfx950
+    correction) and the profile it comes from, or (None, None)."""
+    name, d = _pmc_profile(wl, shape)
+    if d and d.get("hbm_bytes_per_launch"):
+        return float(d["hbm_bytes_per_launch"]["total"]), name
+    return None, None
 
 
 def launch_ranks(gpus: int) -> int:
@@ -181,6 +184,8 @@ def launch_ranks(gpus: int) -> int:
 
 def main():
     args = parse()
+    if args.gpus is None:  # `torchrun --nproc-per-node N bench.py` without --gpus: the launcher's world
+        args.gpus = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
     import torch
@@ -438,10 +443,12 @@ def main():
     gcups = total_cells / elapsed / 1e9
     if rank == 0:
         kern_gcups = cells_per_step / (kern_ms * 1e-3) / 1e9
+        shape = f"pairs={len(qs)}" if wl == "c4" else f"{m},{n}"
+        traffic, traffic_src = load_traffic(wl, shape)
         if wl in BYTES_PER_CELL:
             achieved = BYTES_PER_CELL[wl] * kern_gcups
             roof = dict(bound="hbm", achieved=round(achieved, 2), peak=HBM_PEAK_GBS, unit="GB/s",
-                        frac=round(achieved / HBM_PEAK_GBS, 4), traffic=load_traffic(wl),
+                        frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic, traffic_source=traffic_src,
                         note=f"algorithmic bytes = {BYTES_PER_CELL[wl]:.0f} B/cell x {cells_per_step} cells per "
                              f"launch / DP-kernel mean time {kern_ms:.4f} ms (HIP events on the launch stream); "
                              f"traffic = committed PMC HBM bytes per launch. The kernel is bound by the "
@@ -450,10 +457,10 @@ def main():
             achieved = OPS_PER_CELL[wl] * kern_gcups / 1000.0
             roof = dict(bound="valu", achieved=round(achieved, 3), peak=round(VALU_PEAK_TOPS, 2),
                         unit="T int32 lane-ops/s", frac=round(achieved / VALU_PEAK_TOPS, 4),
-                        traffic=load_traffic(wl),
+                        traffic=traffic, traffic_source=traffic_src,
                         note=f"algorithmic ops = {OPS_PER_CELL[wl]:.0f} int32 ops/cell (SURVEY §8(d)) x cells / "
                              f"DP-kernel mean time {kern_ms:.4f} ms; peak = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz")
-        roof["pmc_wave_time"] = load_wave_time(wl)
+        roof["pmc_wave_time"] = load_wave_time(wl, shape)
         cpu = None
         if not args.no_cpu_baseline:
             try:

@@ -74,6 +74,8 @@ def lib() -> C.CDLL:
     L.msa_status_string.argtypes = [C.c_int]
     L.msa_version.restype = C.c_int
     L.msa_device_count.argtypes = [C.POINTER(C.c_int)]
+    L.msa_set_device_budget.argtypes = [C.c_int64]
+    L.msa_device_budget_info.argtypes = [C.POINTER(C.c_int64)]
     L.msa_main_alignment.argtypes = [P, P, sz, sz, sz, C.c_double, C.c_double, P, sz, C.POINTER(sz),
                                      C.POINTER(C.c_double)]
     L.msa_subproblem.argtypes = [P, P, sz, sz, sz, sz, C.c_int, C.c_int, C.c_double, C.c_double, P, P, P, P, sz,
@@ -99,6 +101,7 @@ def lib() -> C.CDLL:
     L.msa_plan_results.argtypes = [P, P, P]
     L.msa_plan_error.argtypes = [P, C.POINTER(C.c_int), P]
     L.msa_plan_run_info.argtypes = [P, P, P]
+    L.msa_plan_launch_info.argtypes = [P, P]
     L.msa_plan_clear_error.argtypes = [P, P]
     L.msa_plan_scores.argtypes = [P, P, P]
     L.msa_plan_stripe_meta.argtypes = [P, P, i64, P]
@@ -129,12 +132,12 @@ class _Bind:
 
 # Every symbol include/msa.h declares (checked by the CPU test suite).
 EXPORTED = [
-    "msa_status_string", "msa_version", "msa_device_count", "msa_main_alignment", "msa_subproblem",
+    "msa_status_string", "msa_version", "msa_device_count", "msa_set_device_budget", "msa_device_budget_info", "msa_main_alignment", "msa_subproblem",
     "msa_non_parallel_tables", "msa_optimal_alignment", "msa_main_alignment_partitioned",
     "msa_subproblem_f64", "msa_subproblem_row",
     "msa_partial_partition", "msa_partial_tables", "msa_plan_create", "msa_plan_destroy", "msa_plan_cells_size",
     "msa_plan_run", "msa_plan_results", "msa_plan_error", "msa_plan_run_info", "msa_plan_clear_error", "msa_plan_scores",
-    "msa_plan_stripe_meta", "msa_plan_stripes", "msa_plan_pair_layout",
+    "msa_plan_stripe_meta", "msa_plan_stripes", "msa_plan_pair_layout", "msa_plan_launch_info",
     "msa_plan_checksum", "msa_plan_traceback", "msa_plan_traceback_gotoh",
     "msa_plan_last_kernel_ms", "msa_plan_set_timing", "msa_encode_pair", "msa_sw_align",
 ]

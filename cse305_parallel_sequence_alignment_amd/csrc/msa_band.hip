@@ -259,12 +259,12 @@ __global__ __launch_bounds__((BK_W + 1) * 64) void band_kernel(KArgs a) {
         }
         if (!any) {
           __builtin_amdgcn_s_sleep(FL_IOSLEEP);
-          if (++spins > FL_SPIN_MAX) {
-            if (lane == 0) atomicExch(a.err, 30);
-            break;
-          }
+          if (++spins > FL_SPIN_MAX) break;
         }
       }
+      // (reported after the loop: a divergent store inside it would make the wait loop's control flow
+      // exec-mask based -- tests/test_host.py::test_wait_loops_are_wave_uniform)
+      if (spins > FL_SPIN_MAX && lane == 0) atomicExch(a.err, 30);
     } else if (w < ns) {
       // =================== compute wave: stripe k ===================
       const int k = k0 + w;

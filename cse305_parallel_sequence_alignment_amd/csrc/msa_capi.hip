@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
+#include <condition_variable>
 #include <mutex>
 #include <new>
 #include <string>
@@ -175,6 +176,107 @@ DevPool& dev_pool() {
   return *p;
 }
 
+// Admission control at the drop-in boundary.  The reference's callers run main_alignment_function
+// from hardware_concurrency threads at once, each on whole sequences (testing.cpp:209-287, call at
+// :261; :295-369, call at :345): on a 256-thread host, a 97k pair's ~13 GB footprint (1 B/cell
+// direction bytes + pass-2 inputs) times the callers in flight exceeds any device.  Every host-pointer
+// entry point therefore reserves its call's device footprint (estimated from m, n before anything
+// is allocated: a call never holds part of its memory while it waits) against a per-device budget and
+// waits -- FIFO, so no caller is overtaken -- until it fits.  A call larger than the whole budget
+// runs alone (it waits until nothing else is admitted).  Budget: MSA_DEVICE_BUDGET_MB, else 90% of
+// the device's memory; msa_set_device_budget overrides it at run time.
+class Admission {
+ public:
+  void acquire(int dev, size_t bytes) {
+    std::unique_lock<std::mutex> lk(mu_);
+    Dev& d = get(dev);
+    const uint64_t t = d.next++;
+    bool waited = false;
+    cv_.wait(lk, [&] {
+      const bool ok = d.serving == t && (d.inuse == 0 || d.inuse + bytes <= d.budget);
+      waited = waited || !ok;
+      return ok;
+    });
+    d.inuse += bytes;
+    d.peak = std::max(d.peak, d.inuse);
+    d.admitted++;
+    if (waited) d.waits++;
+    d.serving++;
+    cv_.notify_all();  // the next ticket may fit too
+  }
+  void release(int dev, size_t bytes) {
+    std::lock_guard<std::mutex> lk(mu_);
+    Dev& d = get(dev);
+    d.inuse -= std::min(bytes, d.inuse);
+    cv_.notify_all();
+  }
+  void set_budget(int dev, size_t bytes) {
+    std::lock_guard<std::mutex> lk(mu_);
+    Dev& d = get(dev);
+    d.budget = bytes ? bytes : default_budget(dev);
+    d.peak = d.inuse;
+    d.waits = d.admitted = 0;
+    cv_.notify_all();
+  }
+  void info(int dev, int64_t* out) {
+    std::lock_guard<std::mutex> lk(mu_);
+    Dev& d = get(dev);
+    out[0] = (int64_t)d.budget;
+    out[1] = (int64_t)d.inuse;
+    out[2] = (int64_t)d.peak;
+    out[3] = (int64_t)d.waits;
+    out[4] = (int64_t)d.admitted;
+  }
+
+ private:
+  struct Dev {
+    bool init = false;
+    size_t budget = 0, inuse = 0, peak = 0;
+    uint64_t next = 0, serving = 0, waits = 0, admitted = 0;
+  };
+  static size_t default_budget(int dev) {
+    const char* e = std::getenv("MSA_DEVICE_BUDGET_MB");
+    if (e && std::atoll(e) > 0) return (size_t)std::atoll(e) << 20;
+    size_t fr = 0, tot = 0;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    if (cur != dev) (void)hipSetDevice(dev);
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) { (void)hipGetLastError(); tot = size_t(16) << 30; }
+    if (cur != dev) (void)hipSetDevice(cur);
+    return tot / 10 * 9;
+  }
+  Dev& get(int dev) {  // (mu_ held)
+    Dev& d = dev_[dev];
+    if (!d.init) {
+      d.init = true;
+      d.budget = default_budget(dev);
+    }
+    return d;
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::map<int, Dev> dev_;
+};
+
+Admission& admission() {
+  static Admission* a = new Admission();
+  return *a;
+}
+
+// RAII reservation of one call's device footprint (declare it before the call's streams and blocks:
+// destroyed last, after they have been synchronized and returned)
+struct Admit {
+  int dev = 0;
+  size_t bytes = 0;
+  explicit Admit(size_t b) : bytes(b) {
+    (void)hipGetDevice(&dev);
+    admission().acquire(dev, bytes);
+  }
+  ~Admit() { admission().release(dev, bytes); }
+  Admit(const Admit&) = delete;
+  Admit& operator=(const Admit&) = delete;
+};
+
 // Non-blocking streams reused across calls (creating one costs ~10s of us), one
 // free list per device: a stream is only handed to a caller whose current device
 // created it.
@@ -242,20 +344,37 @@ int device_cus() {
   cus[dev] = n;
   return n;
 }
+// LDS a workgroup may allocate on the current device: min(sharedMemPerBlockOptin, 160 KiB), read once
+// per device (plans reject larger requests instead of failing the attribute call on a smaller part)
+size_t device_lds_max() {
+  static std::map<int, size_t> lds;
+  const int dev = current_device();
+  std::lock_guard<std::mutex> lk(g_shape_mu);
+  auto it = lds.find(dev);
+  if (it != lds.end()) return it->second;
+  hipDeviceProp_t prop;
+  size_t v = 64 * 1024;
+  if (hipGetDeviceProperties(&prop, dev) == hipSuccess)
+    v = std::max<size_t>(prop.sharedMemPerBlockOptin, prop.sharedMemPerBlock);
+  v = std::min<size_t>(v, 160 * 1024);
+  lds[dev] = v;
+  return v;
+}
 // raises the kernel's dynamic-LDS limit to the CU's whole LDS (once per device and kernel: plans of
 // one kernel with different LDS sizes then never lower it under each other) and returns its
 // occupancy at `lds` bytes (blocks per CU, >= 1), or -1
 int kernel_shape(kfn_t fn, int threads, size_t lds) {
   static std::map<std::tuple<int, kfn_t, int, size_t>, int> occ_of;
   static std::map<std::pair<int, kfn_t>, bool> attr_set;
+  const size_t lds_max = device_lds_max();
   const auto key = std::make_tuple(current_device(), fn, threads, lds);
   std::lock_guard<std::mutex> lk(g_shape_mu);
   auto it = occ_of.find(key);
   if (it != occ_of.end()) return it->second;
-  if (lds > 160 * 1024) return -1;
+  if (lds > lds_max) return -1;
   const auto ak = std::make_pair(current_device(), fn);
   if (!attr_set[ak]) {
-    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max) != hipSuccess)
       return -1;
     attr_set[ak] = true;
   }
@@ -455,6 +574,22 @@ const char* msa_status_string(int s) {
 
 int msa_version(void) { return 1; }
 
+int msa_set_device_budget(int64_t bytes) {
+  if (bytes < 0) return MSA_ERR_ARG;
+  int rc = ensure_device();
+  if (rc != MSA_OK) return rc;
+  admission().set_budget(current_device(), (size_t)bytes);
+  return MSA_OK;
+}
+
+int msa_device_budget_info(int64_t* out5) {
+  if (!out5) return MSA_ERR_ARG;
+  int rc = ensure_device();
+  if (rc != MSA_OK) return rc;
+  admission().info(current_device(), out5);
+  return MSA_OK;
+}
+
 int msa_device_count(int* count) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
@@ -570,7 +705,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   const bool got_ok = kalg == MSA_ALG_REF1 && out_mode == MSA_OUT_DIR && 4 * (1 + 2 * desc->gap_extend) <= 127;
   const bool flow = single && ((kalg == MSA_ALG_SWL || kalg == MSA_ALG_SWL0) ?
                                (out_mode == MSA_OUT_H || (out_mode == MSA_OUT_NONE && !tp)) : (aff_ok || got_ok)) &&
-                    desc->m[0] > 0 && flow_lds <= 160 * 1024;
+                    desc->m[0] > 0 && flow_lds <= device_lds_max();
   P->flow = flow;
   P->flow2 = flow && (out_mode == MSA_OUT_H || aff);
   const int W = flow ? FL_W : (single ? MSA_WAVES_SINGLE : MSA_WAVES_BATCH);
@@ -730,8 +865,9 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     // pass-2 blocks: FL_P2INTS ints per wave (inputs + column codes staged in LDS)
     if (P->flow2) P->lds_bytes = std::max(flow_lds, (size_t)(FL_W + 2) * FL_P2INTS * 4);
   }
-  if (P->lds_bytes > 160 * 1024) {
-    std::fprintf(stderr, "msa: problem needs %zu B of LDS per workgroup (> 160 KiB)\n", P->lds_bytes);
+  if (P->lds_bytes > device_lds_max()) {
+    std::fprintf(stderr, "msa: problem needs %zu B of LDS per workgroup (> %zu B, the device's limit)\n",
+                 P->lds_bytes, device_lds_max());
     delete P;
     return MSA_ERR_UNSUPPORTED;
   }
@@ -817,14 +953,18 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     const int S = (m0 + 63) / 64;
     const int L8 = bk_code_bytes(m0, n0, band);
     const size_t blds = bk_lds_bytes(L8);
-    const int bocc = (blds <= 160 * 1024) ? kernel_shape(band_kernel, (BK_W + 1) * 64, blds) : -1;
+    const int bocc = (blds <= device_lds_max()) ? kernel_shape(band_kernel, (BK_W + 1) * 64, blds) : -1;
     if (bocc > 0) {
-      auto env_int = [](const char* name, int dflt) {
-        const char* e = std::getenv(name);
-        return e ? std::atoi(e) : dflt;
-      };
-      const int warm = std::max(0, env_int("MSA_BAND_WARM", kWarm) / BK_W * BK_W);
-      const int cc = std::max(BK_W, env_int("MSA_BAND_CHUNK", 12) / BK_W * BK_W);
+      // diagnostic knobs, read once per process; a warm-up shorter than one item (BK_W stripes) gives
+      // chunk_check nothing to compare (checkpoint slot 2c is never written): chunking is then off
+      static const int warm = [] {
+        const char* e = std::getenv("MSA_BAND_WARM");
+        return std::max(0, (e ? std::atoi(e) : kWarm) / BK_W * BK_W);
+      }();
+      static const int cc = [] {
+        const char* e = std::getenv("MSA_BAND_CHUNK");
+        return std::max(BK_W, (e ? std::atoi(e) : 12) / BK_W * BK_W);
+      }();
       const int nch = (S + cc - 1) / cc;
       msa_kparams ek = kp;  // the exact launch
       ek.single = 1;
@@ -843,7 +983,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
       P->grid = std::max(1, std::min(ek.n_items, ncu * bocc));
       kp = ek;
       P->band_items = ek.n_items;
-      if (nch >= 4 && out_mode == MSA_OUT_H) {
+      if (nch >= 4 && out_mode == MSA_OUT_H && warm >= BK_W) {
         P->chunked = true;
         P->n_chunks = nch;
         P->fb_kp = ek;
@@ -896,7 +1036,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
       P->threads = (MSA_WAVES_BATCH + 1) * 64;
       P->lds_bytes = (16 + (size_t)kp.sched_cap * 8 + (size_t)(2 * MSA_WAVES_BATCH + 1) * P->nc * MSA_RING +
                       (size_t)P->nc * kp.lds_row_words) * 4;
-      const int occ2 = (P->lds_bytes > 160 * 1024) ? -1 : kernel_shape(P->fn, P->threads, P->lds_bytes);
+      const int occ2 = (P->lds_bytes > device_lds_max()) ? -1 : kernel_shape(P->fn, P->threads, P->lds_bytes);
       if (occ2 < 0) {
         delete P;
         return MSA_ERR_UNSUPPORTED;
@@ -1161,6 +1301,21 @@ int msa_plan_run_info(msa_plan* P, int32_t* out4, void* stream) {
     HIPCHK(hipStreamSynchronize(st));
     out4[2] = v;
   }
+  return MSA_OK;
+}
+
+int msa_plan_launch_info(const msa_plan* P, int32_t* out8) {
+  if (!P || !out8) return MSA_ERR_ARG;
+  const int mode = P->band_k ? (P->chunked ? 5 : 4)
+                             : (P->chunked ? 2 : (P->flow ? 1 : (P->kp.single == 3 ? 3 : 0)));
+  out8[0] = mode;
+  out8[1] = P->grid;
+  out8[2] = P->threads;
+  out8[3] = (int32_t)P->lds_bytes;
+  out8[4] = P->nflow;
+  out8[5] = P->fill_fn ? P->fill_grid : 0;
+  out8[6] = P->R;
+  out8[7] = P->kp.n_items;
   return MSA_OK;
 }
 

@@ -665,7 +665,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
         nb = min(nb, consv + FL_RINGB - b);
         if (nb <= 0) {
           if (k0 == 0 || consv + FL_RINGB <= b) __builtin_amdgcn_s_sleep(FL_IOSLEEP);  // (granule polls pace themselves)
-          if (++spins > FL_SPIN_MAX) { if (lane == 0) atomicExch(a.err, 10); break; }
+          if (++spins > FL_SPIN_MAX) break;
           continue;
         }
         // codes for the blocks' next phases must be in LDS before they are published (a full
@@ -675,7 +675,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
           if (Yr < L8) nb = min(nb, (Yr - 192) / 16 - b);
           if (nb <= 0) {
             __builtin_amdgcn_s_sleep(FL_IOSLEEP);
-            if (++spins > FL_SPIN_MAX) { if (lane == 0) atomicExch(a.err, 10); break; }
+            if (++spins > FL_SPIN_MAX) break;
             continue;
           }
         }
@@ -691,6 +691,9 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
         if (lane == 0) lds_vstore(pub, b + nb);
         b += nb;
       }
+      // (a spin limit ends the loop; reported after it: a divergent store inside a wait loop makes the
+      // loop's control flow exec-mask based -- tests/test_host.py::test_wait_loops_are_wave_uniform)
+      if (b <= Bmax && lane == 0) atomicExch(a.err, 10);
     } else if (w == W + 1) {
       // ============ io-out: links' blocks -> BR (pass 2), last link -> granules ============
       int bl[W + 1], bmx[W + 1];
@@ -741,9 +744,10 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
         if (!left) break;
         if (!any) {
           __builtin_amdgcn_s_sleep(FL_IOSLEEP);
-          if (++spins > FL_SPIN_MAX) { if (lane == 0) atomicExch(a.err, 11); break; }
+          if (++spins > FL_SPIN_MAX) break;
         }
       }
+      if (spins > FL_SPIN_MAX && lane == 0) atomicExch(a.err, 11);  // (after the loop, as io-in)
     } else if (k0 + w < S) {
      // (two-value kinds: affine SW and Gotoh share this wave's protocol; the one-value SW-linear
      // wave follows in the else branch)

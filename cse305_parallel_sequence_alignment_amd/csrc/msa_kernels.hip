@@ -588,11 +588,9 @@ __device__ __forceinline__ void loader_commit(const KArgs& a, int cs0, int nch, 
     const unsigned long long r = gload(g_in + (size_t)min(v, NC - 1) * a.gbuf_stride + cc + MSA_GOFF);
     gv = ok ? gv : r;
     ok = !need || ((unsigned)(gv >> 32) == ep);
-    if (++spins > (1u << 24)) {
-      if (lane == 0) atomicExch(a.err, 1);
-      break;
-    }
+    if (++spins > (1u << 24)) break;
   }
+  if (spins > (1u << 24) && lane == 0) atomicExch(a.err, 1);  // (after the loop: a uniform wait loop)
   if (v < NC) stage[v * MSA_RING + ((16 * q + l) & (MSA_RING - 1))] = need ? (int)(unsigned)gv : MSA_NEG;
 }
 
@@ -880,13 +878,11 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
           // phase 0's columns published before anything is loaded
           const int colw = min(min(s0.cs + 16 * (CPP - 1) + 15, chi), n);
           unsigned spins = 0;
-          while ((unsigned)(gload(g_in + colw + MSA_GOFF) >> 32) != ep) {
+          while (uni((int)(unsigned)(gload(g_in + colw + MSA_GOFF) >> 32)) != (int)ep) {
             __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1u << 24)) {
-              if (lane == 0) atomicExch(a.err, 1);
-              break;
-            }
+            if (++spins > (1u << 24)) break;
           }
+          if (spins > (1u << 24) && lane == 0) atomicExch(a.err, 1);
         }
 #pragma unroll
         for (int h = 0; h < CPP; ++h) G[h] = loader_issue<NC>(a, s0.cs, h, g_in, lane);

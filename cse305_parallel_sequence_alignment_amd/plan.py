@@ -135,6 +135,16 @@ class Plan:
         return dict(mode={0: "stripe", 1: "flow", 2: "chunked"}[v[0]], chunks=int(v[1]), converged=int(v[2]),
                     warm_stripes=int(v[3]))
 
+    def launch_info(self) -> dict:
+        """How the plan launches (msa_plan_launch_info): kernel mode, grid, threads, LDS bytes, flow pass-1
+        workgroups, workgroups of the separate pass-2 launch (0 = pass 2 inside the main launch), rows per
+        lane, items."""
+        v = (C.c_int32 * 8)()
+        LB.check(LB.lib().msa_plan_launch_info(self._h, v), "msa_plan_launch_info")
+        modes = {0: "stripe", 1: "flow", 2: "chunked", 3: "split", 4: "band", 5: "band_chunked"}
+        return dict(mode=modes[v[0]], grid=int(v[1]), threads=int(v[2]), lds_bytes=int(v[3]), nflow=int(v[4]),
+                    fill_grid=int(v[5]), rows_per_lane=int(v[6]), items=int(v[7]))
+
     def clear_error(self, stream=None) -> None:
         LB.check(LB.lib().msa_plan_clear_error(self._h, _stream_ptr(stream)), "msa_plan_clear_error")
 

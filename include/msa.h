@@ -58,6 +58,19 @@ int msa_version(void);
 /* number of usable gfx950 devices */
 int msa_device_count(int* count);
 
+/* Admission control of the host-pointer entry points (msa_main_alignment, msa_subproblem,
+ * msa_partial_*, msa_sw_align, msa_optimal_alignment's subproblems).  The reference's callers
+ * run main_alignment_function from hardware_concurrency threads at once on whole sequences
+ * (test_functions/testing.cpp:269-280 and :352-358, calls at :261 and :345); every call here
+ * reserves its estimated device footprint against a per-device budget before allocating and
+ * waits (FIFO) until it fits, instead of failing with MSA_ERR_NOMEM.  A call larger than the
+ * budget runs alone.  Budget: env MSA_DEVICE_BUDGET_MB, else 90% of device memory;
+ * msa_set_device_budget(bytes) sets it for the current device (0 = back to the default).
+ * msa_device_budget_info: out5 = {budget, bytes admitted now, peak admitted bytes since the
+ * last set, calls that had to wait, calls admitted}. */
+int msa_set_device_budget(int64_t bytes);
+int msa_device_budget_info(int64_t* out5);
+
 /* Node of an alignment path: the reference's `align` struct
  * (subproblem_alignment.h:8-13) without the `next` pointer. */
 typedef struct msa_node {
@@ -226,6 +239,13 @@ int msa_plan_results(msa_plan* plan, msa_pair_result* out, void* stream);
  * launch recomputed them; -1 otherwise), warm-up stripes per chunk}.
  * Synchronizes `stream` for mode 2. */
 int msa_plan_run_info(msa_plan* plan, int32_t* out4, void* stream);
+/* How the plan launches (for tests and tools): out8 = {mode: 0 stripe_kernel (batch), 1 flow_kernel
+ * (single pair, two-pass), 2 chunked banded stripe_kernel, 3 split batch (every pair split into items
+ * over several CUs), 4 band_kernel exact chain, 5 band_kernel chunked; workgroups of the main launch;
+ * threads per workgroup; dynamic LDS bytes; flow pass-1 workgroups; workgroups of the separate pass-2
+ * launch (flow_fill_kernel, long pairs; 0 = pass 2 runs inside the main launch); rows per lane;
+ * items}. */
+int msa_plan_launch_info(const msa_plan* plan, int32_t* out8);
 /* The sticky error word (0 = no error; else the kernel site code), synchronizes. */
 int msa_plan_error(msa_plan* plan, int* code, void* stream);
 /* Reset the sticky error word (stream-ordered). */

@@ -26,21 +26,23 @@ elif wl == "c5":
     A, B = data.c5_pair(0, False)  # the bench's C5 pair
     pl = Plan(LB.SW_AFFINE, LB.CELLS_DIR, [20000], [20000], [0], [0], match=1, mismatch=0, gap_open=3,
               gap_extend=1, track_end=True)
-elif wl in ("ref", "ref20"):
-    L = 10000 if wl == "ref" else 20000
-    A, B = seqs[0][:L], seqs[1][:L]  # the bench's ref pair (main_alignment_function's path)
-    pl = Plan(LB.REF_GOTOH, LB.CELLS_DIR, [L], [L], [0], [0], match=1, mismatch=0, gap_open=3, gap_extend=1,
-              start_type=-1)
+elif wl in ("ref", "ref20", "refwhole"):
+    L = {"ref": 10000, "ref20": 20000, "refwhole": None}[wl]
+    # the bench's ref pairs (main_alignment_function's path); refwhole = bench --ref-pair 3,4 --ref-len 0
+    A, B = (seqs[0][:L], seqs[1][:L]) if L else (seqs[3], seqs[4])
+    L = len(A)
+    pl = Plan(LB.REF_GOTOH, LB.CELLS_DIR, [len(A)], [len(B)], [0], [0], match=1, mismatch=0, gap_open=3,
+              gap_extend=1, start_type=-1)
 elif wl == "c3":
     from cse305_parallel_sequence_alignment_amd import data
 
     A, B = data.c3_pair(False)
     pl = Plan(LB.NW_BANDED, LB.CELLS_H, [len(A)], [len(B)], [0], [0], match=1, mismatch=0, gap_open=3,
               gap_extend=1, band=512)
-else:  # c4
-    L, K = 4000, 1024
+else:  # c4 (1024 pairs) / c4_128 (the first 128: one rank's share at 8 GPUs, split mode)
+    L, K = 4000, (128 if wl == "c4_128" else 1024)
     rng = np.random.default_rng(0x5EED0004)
-    offs = rng.integers(0, 13309 - L, size=K)
+    offs = rng.integers(0, 13309 - L, size=1024)  # the same windows as data.c4_offsets()
     A = b"".join(seqs[k % 20][offs[k]:offs[k] + L] for k in range(K))
     B = seqs[0][:L]
     pl = Plan(LB.SW_LINEAR, LB.CELLS_NONE, [L] * K, [L] * K, [k * L for k in range(K)], [0] * K, match=1,
@@ -49,7 +51,7 @@ if pl.cells != LB.CELLS_NONE:
     out = torch.empty(pl.cells_elems, dtype=torch.uint8 if pl.cells == LB.CELLS_DIR else torch.int32, device="cuda")
 dA, dB = enc(A), enc(B)
 tb = None
-if wl in ("c5", "ref", "ref20"):  # the bench's step: fill, then the traceback walk on the device
+if wl in ("c5", "ref", "ref20", "refwhole"):  # the bench's step: fill, then the traceback walk on the device
     tb = (torch.empty(len(A) + len(B) + 2, dtype=torch.uint8, device="cuda"),
           torch.zeros(8, dtype=torch.int64, device="cuda"))
 for _ in range(reps):

@@ -900,6 +900,72 @@ def test_flow_kernels_wide_pairs(oracle, dev, LB, m, n):
     assert pl.checksum(H) == oracle.checksum_h(o["H"])
 
 
+@pytest.mark.parametrize("kind", ["swl_h", "swl_h_end", "swa_nneg", "swa_neg", "gotoh"])
+def test_flow_fill_launch_tall_pairs(oracle, dev, LB, kind):
+    """Tall-narrow pairs (70,000 x 300: ~137 pass-1 items, more flow workgroups than half the CUs) take the
+    separate pass-2 launch (flow_fill_kernel, launch_info fill_grid > 0), whose instantiation pick_fill
+    chooses per algorithm: SW linear with H (track_end off / on), SW affine with direction bytes (scores
+    >= 0, and with a negative mismatch) and the reference's Gotoh.  Checked against the oracle: H checksum
+    and score; score, end, begin and CIGAR of the device traceback; the printed alignment text."""
+    import torch
+    from cse305_parallel_sequence_alignment_amd import api
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+
+    m, n = 70000, 300
+    rng = np.random.default_rng(7000 + len(kind))
+    A = rs(rng, m)
+    B = bytearray(A[20000:20000 + n])  # a local match deep in A, mutated
+    for k in rng.choice(n, size=n // 12, replace=False):
+        B[k] = ACGT[rng.integers(4)]
+    B = bytes(B)
+    dA, dB = _dev(A, dev), _dev(B, dev)
+    if kind.startswith("swl"):
+        te = kind == "swl_h_end"
+        pl = Plan(LB.SW_LINEAR, LB.CELLS_H, [m], [n], [0], [0], match=1, mismatch=0, gap_open=1, gap_extend=1,
+                  track_end=te)
+        info = pl.launch_info()
+        assert info["mode"] == "flow" and info["fill_grid"] > 0, info
+        H = torch.empty(pl.cells_elems, dtype=torch.int32, device=dev)
+        pl.run(dA, dB, H)
+        o = oracle.sw(A, B, 1, 0, 1, 1, want_h=True)
+        r = pl.results()[0]
+        assert r["score"] == o["score"]
+        if te:
+            assert tuple(r["end"]) == tuple(o["end"])
+        assert pl.checksum(H) == oracle.checksum_h(o["H"])
+    elif kind.startswith("swa"):
+        sc = (1, 0, 3, 1) if kind == "swa_nneg" else (2, -3, 5, 2)
+        pl = Plan(LB.SW_AFFINE, LB.CELLS_DIR, [m], [n], [0], [0], match=sc[0], mismatch=sc[1], gap_open=sc[2],
+                  gap_extend=sc[3], track_end=True)
+        info = pl.launch_info()
+        assert info["mode"] == "flow" and info["fill_grid"] > 0, info
+        D = torch.empty(pl.cells_elems, dtype=torch.uint8, device=dev)
+        pl.run(dA, dB, D)
+        tb = pl.traceback(D)
+        o = oracle.sw(A, B, *sc, want_tb=True)
+        r = pl.results()[0]
+        assert (r["score"], tuple(r["end"]), tuple(tb["beg"]), tb["cigar"]) == \
+            (o["score"], tuple(o["end"]), tuple(o["beg"]), o["cigar"])
+    else:
+        pl = Plan(LB.REF_GOTOH, LB.CELLS_DIR, [m], [n], [0], [0], match=1, mismatch=0, gap_open=3, gap_extend=1,
+                  start_type=-1)
+        info = pl.launch_info()
+        assert info["mode"] == "flow" and info["fill_grid"] > 0, info
+        D = torch.empty(pl.cells_elems, dtype=torch.uint8, device=dev)
+        pl.run(dA, dB, D)
+        # the oracle's Subproblem swaps a tall pair (m > n, subproblem_alignment.h:37-54); the symmetric
+        # recurrence makes the unswapped tables its transposes with T2 <-> T3: T1' = T1^T, T2' = T3^T,
+        # T3' = T2^T -- the tables of this (unswapped) plan
+        T1, T2, T3, inv = oracle.subproblem_tables(A, B, -1, 1.0, 2.0)
+        assert inv
+        T1, T2, T3 = T1.T.copy(), T3.T.copy(), T2.T.copy()
+        r = pl.results()[0]
+        assert tuple(float(x) for x in r["fin"]) == tuple(float(T[m, n]) for T in (T1, T2, T3))
+        d = pl.deskew_dir(D.cpu().numpy(), 0, pl.stripe_meta())
+        assert np.array_equal(d[1:, 1:] & 63, _gotoh_tags(T1, T2, T3, 1.0, 2.0))
+    assert pl.error() == 0
+
+
 @pytest.mark.parametrize("how", ["batch_of_one", "g16_single"])
 def test_ref1_stripe_layout_walk(oracle, dev, LB, how):
     """The tagged REF1 fill in the one-pass stripe kernel (a one-pair batch, or a single pair whose profile bytes

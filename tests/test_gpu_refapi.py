@@ -167,6 +167,43 @@ def test_concurrent_main_alignment_at_size(dev, dataset):
         assert (sc, md5) == (c["score"], c["lines_md5"]), c
 
 
+def test_concurrent_main_alignment_under_budget(dev, dataset):
+    """Admission control at the drop-in boundary (the reference's callers run main_alignment_function from
+    hardware_concurrency threads on whole sequences, testing.cpp:269-280 / :352-358): 8 threads x 20k calls
+    under a 1 GB device budget -- one call's footprint (~0.58 GB) fits, two do not -- so the calls queue on
+    the budget instead of failing; every status is OK and every text equals the reference's own output."""
+    import ctypes as C
+    import hashlib
+
+    from cse305_parallel_sequence_alignment_amd import _lib as LB, api
+
+    _, seqs = dataset
+    cases = [c for c in json.loads((GOLDEN / "at_size.json").read_text()) if c["L"] == 20000] * 4
+    assert len(cases) >= 8
+    L = LB.lib()
+    budget = 1 << 30
+    LB.check(L.msa_set_device_budget(budget), "msa_set_device_budget")
+    try:
+        def one(c):
+            A, B = seqs[c["a"]][:c["L"]], seqs[c["b"]][:c["L"]]
+            t, sc = api.main_alignment_text(b"\0" + A, b"\0" + B, c["L"], c["L"], 32, c["g"], c["h"])
+            lines = t.split("\n")[5:7]
+            return sc, hashlib.md5((lines[0] + "\n" + lines[1] + "\n").encode()).hexdigest()
+
+        with ThreadPoolExecutor(max_workers=8) as ex:
+            got = list(ex.map(one, cases))
+        info = (C.c_int64 * 5)()
+        LB.check(L.msa_device_budget_info(info), "msa_device_budget_info")
+    finally:
+        L.msa_set_device_budget(0)
+    for (sc, md5), c in zip(got, cases):
+        assert (sc, md5) == (c["score"], c["lines_md5"]), c
+    b, inuse, peak, waits, admitted = list(info)
+    assert b == budget and inuse == 0 and admitted == len(cases)
+    assert peak <= budget, (peak, budget)  # never two 20k calls admitted at once
+    assert waits >= 1
+
+
 # ---- the reference's class Subproblem through libmsa_compat.so (C++ drop-in) ----
 
 ROOT = GOLDEN.parent.parent

@@ -193,3 +193,51 @@ def test_harness_similarity_and_reader():
             assert harness.sequence_similarity(s1, s2, T) == _similarity_reference_loop(s1, s2, T)
     assert harness.sequence_similarity(b"ACGTACGTAC", b"ACGAACGTAA", 4) == _similarity_reference_loop(
         b"ACGTACGTAC", b"ACGAACGTAA", 4)
+
+
+def _waitloops():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("waitloops", ROOT / "scripts" / "waitloops.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_wait_loop_detector_flags_exec_controlled_loops():
+    """The detector itself, on a hand-written disassembly: a spin loop closed by s_cbranch_execnz (the
+    divergent-loop lowering) is flagged, the same loop closed by s_cbranch_scc1 is not, and a lane-strided
+    inner loop without a sleep does not count."""
+    W = _waitloops()
+
+    def fn(back):
+        return [(0x100, "s_nop", "0 "), (0x104, "global_load_dwordx2", "v[0:1], v[2:3], off "),
+                (0x108, "v_cmp_ne_u32_e32", "vcc, s4, v1 "), (0x10c, "s_sleep", "1 "),
+                (0x110, "s_and_b64", "exec, exec, vcc "), (0x114, back, "-4 <f+0x4>"),
+                (0x118, "s_endpgm", " ")]
+
+    bad = W.violations(fn("s_cbranch_execnz"))
+    assert len(bad) == 1 and bad[0]["branch"] == "s_cbranch_execnz"
+    assert W.violations(fn("s_cbranch_scc1")) == []
+    inner = [(0x100, "s_sleep", "1 "), (0x104, "v_add_u32_e32", "v0, 64, v0 "),
+             (0x108, "s_cbranch_execnz", "-2 <f+0x4>"), (0x10c, "s_cbranch_scc1", "-4 <f+0x0>")]
+    assert W.violations(inner) == []
+
+
+def test_wait_loops_are_wave_uniform():
+    """Every spin-wait loop (a loop around an s_sleep) of every kernel in libmsa.so's gfx950 code object
+    closes and exits on scalar state (s_branch / s_cbranch_scc* / s_cbranch_vcc*), never on the exec
+    mask.  Rounds 3 and 4 each hung a GPU run when codegen turned such a loop divergent (an inlined
+    block body; a spin-limit error store inside the loop); this guards the flow kernels, the band
+    kernel, the pass-2 block bodies and the stripe kernel's loader against it from the CPU suite."""
+    W = _waitloops()
+    so = ROOT / "cse305_parallel_sequence_alignment_amd" / "libmsa.so"
+    if not so.exists():
+        pytest.skip("libmsa.so not built")
+    res = W.scan(so)
+    with_loops = {k: v for k, v in res.items() if v["loops"]}
+    for prefix in ("_ZN3msa11flow_kernel", "_ZN3msa11band_kernel", "_ZN3msa13stripe_kernel",
+                   "_ZN3msa10fill_block", "_ZN3msa14fill_block_aff", "_ZN3msa14fill_block_got"):
+        assert any(k.startswith(prefix) for k in with_loops), f"no wait loop found in {prefix}*"
+    bad = {k: v["bad"] for k, v in with_loops.items() if v["bad"]}
+    assert not bad, f"exec-mask controlled wait loops: {bad}"
