@@ -23,6 +23,7 @@
 #include "../../include/msa.h"
 #include "msa_kernels.hip"
 #include "msa_flow.hip"
+#include "msa_cflow.hip"
 #include "msa_band.hip"
 #include "msa_rowsweep.hip"
 #include "msa_traceback.hip"
@@ -489,6 +490,7 @@ struct msa_plan {
   bool band_k = false;  // band_kernel (banded single pair, msa_band.hip)
   int band_items = 0;   // band_kernel: items of the larger of its launches (granule slots)
   bool flow2 = false;  // + pass-2 blocks inside the same launch (O_H)
+  bool cflow = false;  // cflow_kernel: packed-couple score-only batch as flag-synchronised chains
   kfn_t fill_fn = nullptr;  // long pairs: pass 2 as a launch of its own behind pass 1
   int fill_grid = 0;
   size_t fill_lds = 0;
@@ -855,10 +857,42 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
       }
     }
   }
+  // Packed score-only batches (C4): cflow_kernel (msa_cflow.hip) -- items of CF_W stripes of one couple,
+  // chained through granules, claimed item-major -- when the couples' code rows fit LDS.  MSA_C4_KERNEL=
+  // lockstep (diagnostic) keeps stripe_kernel's lock-step batch / split modes.
+  if (kalg == MSA_ALG_SWLP && !single) {
+    static const bool lockstep = [] {
+      const char* e = std::getenv("MSA_C4_KERNEL");
+      return e && std::strcmp(e, "lockstep") == 0;
+    }();
+    int64_t nmax = 0, mmax = 0;
+    for (int64_t p = 0; p < desc->n_pairs; ++p) {
+      nmax = std::max(nmax, desc->n[p]);
+      mmax = std::max(mmax, desc->m[p]);
+    }
+    const int L8 = fl_code_bytes((int)nmax);
+    const size_t clds = (size_t)(FL_FLAGS + (CF_W + 1) * 256) * 4 + (size_t)FL_NCOPY * (L8 + 16);
+    if (!lockstep && clds <= 96 * 1024) {
+      P->cflow = true;
+      P->fn = cflow_kernel<CF_W>;
+      P->W = CF_W;
+      P->KS = 16;
+      P->threads = (CF_W + 2) * 64;
+      kp.single = 0;
+      kp.lds_code_bytes = L8;
+      kp.code_whole = 1;
+      const int ncpl = (int)((desc->n_pairs + 1) / 2);
+      const int G = (int)(((mmax + 63) / 64 + CF_W - 1) / CF_W);
+      kp.n_items = ncpl * G;
+      kp.sched_cap = 0;
+      kp.lds_row_words = 0;
+    }
+  }
   const size_t lds_ints = 16 + (size_t)kp.sched_cap * 8 + (size_t)(2 * W + 1) * P->nc * MSA_RING +
                           (size_t)P->nc * kp.lds_row_words +
                           (single ? (size_t)4 * (MSA_CRING / 4 + 16) : 0);  // code ring
   P->lds_bytes = lds_ints * 4;
+  if (P->cflow) P->lds_bytes = (size_t)(FL_FLAGS + (CF_W + 1) * 256) * 4 + (size_t)FL_NCOPY * (kp.lds_code_bytes + 16);
   if (flow) {
     kp.lds_code_bytes = fl_code_bytes((int)desc->n[0]);
     P->lds_bytes = flow_lds;
@@ -877,7 +911,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     return MSA_ERR_HIP;
   }
   const int ncu = device_cus();
-  const int cap = ncu * std::min(occ, 2);
+  const int cap = ncu * (P->cflow ? occ : std::min(occ, 2));
   P->grid = std::max(1, std::min(kp.n_items, cap));
   if (flow) {
     // Items go to the 8 XCDs in runs of G consecutive items, round-robin (workgroup b takes
@@ -1070,6 +1104,14 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     // band_kernel: item t publishes (Z, F~) of its last row into slot t (chunked and exact launches)
     P->gbuf_stride = (int)(((desc->n[0] + 2 * MSA_GOFF + 16) + 15) & ~15);
     const size_t gb = (size_t)P->band_items * 2 * P->gbuf_stride * sizeof(unsigned long long);
+    if (!P->alloc(&P->d_gbuf, gb)) return fail();
+    if (hipMemset(P->d_gbuf, 0, gb) != hipSuccess) return fail();
+  } else if (P->cflow) {
+    // cflow_kernel: item t publishes the last link of its stripes into slot t (read by item t + couples)
+    int64_t nmax = 0;
+    for (int64_t p = 0; p < desc->n_pairs; ++p) nmax = std::max(nmax, desc->n[p]);
+    P->gbuf_stride = (int)(((nmax + 2 * MSA_GOFF + 16) + 15) & ~15);
+    const size_t gb = (size_t)kp.n_items * P->gbuf_stride * sizeof(unsigned long long);
     if (!P->alloc(&P->d_gbuf, gb)) return fail();
     if (hipMemset(P->d_gbuf, 0, gb) != hipSuccess) return fail();
   } else if ((single || kp.single == 3) && single_items > 1) {
@@ -1306,7 +1348,7 @@ int msa_plan_run_info(msa_plan* P, int32_t* out4, void* stream) {
 
 int msa_plan_launch_info(const msa_plan* P, int32_t* out8) {
   if (!P || !out8) return MSA_ERR_ARG;
-  const int mode = P->band_k ? (P->chunked ? 5 : 4)
+  const int mode = P->cflow ? 6 : P->band_k ? (P->chunked ? 5 : 4)
                              : (P->chunked ? 2 : (P->flow ? 1 : (P->kp.single == 3 ? 3 : 0)));
   out8[0] = mode;
   out8[1] = P->grid;

@@ -290,6 +290,7 @@ struct LaneState {
   int LB[3];   // left border held while t < tmin
   int tmin, tmax;
   int best, bt;  // SW best in this lane's row and the step it first occurred
+  int pb;        // SWLP: max over the current phase's steps k of G - g k (both pairs, int16)
   int fin[3];
   unsigned plo, phi;  // substitution profile (8 int8 scores by column code)
   int i;              // DP row
@@ -323,10 +324,11 @@ __device__ __forceinline__ unsigned step(const msa_kparams& kp, LaneState<ALG>& 
     asm("" : "+v"(nS[0]));
     L.U[0] = up;
   } else if constexpr (ALG == MSA_ALG_SWLP) {
-    // MSA_ALG_SWL0 on two pairs at once: s holds both pairs' score + 2g as int16
+    // MSA_ALG_SWL0 on two pairs at once: s holds both pairs' score + 2g as int16.  The cell above (the
+    // DPP from lane r-1) enters last: the loop-carried path per step is DPP -> one v_pk_max_i16, the
+    // diagonal-left max runs in the DPP's wait states
     const int up = dpp_shr1(in[0], L.S[0]);
-    nS[0] = pk_max(pk_max(pk_add(L.U[0], s), up), L.S[0]);
-    asm("" : "+v"(nS[0]));
+    nS[0] = pk_max(pk_max(pk_add(L.U[0], s), L.S[0]), up);
     L.U[0] = up;
   } else if constexpr (ALG == MSA_ALG_SWL0) {
     // all scores >= 0: G(i-1,j-1) + s + 2g >= g*(i+j) whenever the diagonal
@@ -452,10 +454,12 @@ __device__ __forceinline__ unsigned step(const msa_kparams& kp, LaneState<ALG>& 
     }
   } else {
     if constexpr (pk16(ALG)) {
+      // ct = pk2(-g k) for step k of the phase (an SGPR fixed for the whole launch): the phase's best
+      // of G - g k in both halves; the phase's g (i + j) at its step 0 is subtracted once per phase
+      // (run_phase), so no scalar arithmetic runs per step
       static_assert(TRACKPOS == 0, "packed pairs: score only");
-      const int hv = pk_add(nS[0], pk2(-ct));  // both pairs' H = G - g(i+j)
-      hout = hv;
-      L.best = pk_max(L.best, hv);
+      L.pb = pk_max(L.pb, pk_add(nS[0], ct));
+      hout = 0;
     } else if constexpr (swlin(ALG) || ALG == MSA_ALG_SWA) {
       const int hv = swlin(ALG) ? nS[0] - ct : nS[0];
       hout = hv;
@@ -948,7 +952,16 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
       }
       L.best = 0;
       L.bt = -1;
+      L.pb = (int)0x80008000u;
       const int gdiag = kp.gap_open * (64 * ks + 1 + sg.cs);  // SWL: g*(i+j) at step 0, same for all lanes
+      // SWLP: pk2(-g k) per step k of a phase, wave-uniform and fixed for the launch (opaque: computed
+      // once per stripe instead of rematerialized at every step)
+      int gkp[KS];
+#pragma unroll
+      for (int k = 0; k < KS; ++k) {
+        gkp[k] = pk16(ALG) ? pk2(-kp.gap_open * k) : 0;
+        if constexpr (pk16(ALG)) asm("" : "+s"(gkp[k]));
+      }
       // SWL: the lane starts left of the matrix on virtual cells with H = 0,
       // i.e. G = g*(i+j); its left neighbour at step 0 is G = gdiag - g
       if constexpr (swlin(ALG)) {
@@ -997,6 +1010,11 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
       // batch: codes of phase q+1 are loaded during phase q (global loads);
       // single pair: read from the loader-staged LDS ring at phase start
       unsigned cwn[KS / 4];
+      // packed batches (C4): codes two phases ahead (cwn = phase q+1, cwn2 = phase q+2): one phase of
+      // lock-step computing did not cover a global load's latency (stamps: ~0.3 us of a 1.04 us phase
+      // waited for the codes)
+      constexpr bool CPF2 = pk16(ALG) && !LDSCODE;
+      unsigned cwn2[KS / 4];
       const int cj0 = sg.cs - lane;                // column of this lane at step 0
       const unsigned* cr_base = cring + (cj0 & 3) * CRW;
       const int cd0 = cj0 >> 2;                    // floor: absolute dword index at step 0
@@ -1005,6 +1023,15 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
           const unsigned* cp = cr_base + ((cd0 + (KS / 4) * q) & (MSA_CRING / 4 - 1));
 #pragma unroll
           for (int u = 0; u < KS / 4; ++u) cwn[u] = cp[u];
+        } else if constexpr (CPF2) {
+          // (a phase past the stripe's last reads the padded copy: the padding covers KS/4 dwords)
+#pragma unroll
+          for (int u = 0; u < KS / 4; ++u) cwn[u] = cwn2[u];
+#pragma unroll
+          for (int u = 0; u < KS / 4; u += 4) {
+            const uint4 c4 = *reinterpret_cast<const uint4*>(cptr + (KS / 4) * (q + 1) + u);
+            cwn2[u] = c4.x; cwn2[u + 1] = c4.y; cwn2[u + 2] = c4.z; cwn2[u + 3] = c4.w;
+          }
         } else {
 #pragma unroll
           for (int u = 0; u < KS / 4; u += 4) {
@@ -1013,7 +1040,16 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
           }
         }
       };
-      if constexpr (!LDSCODE) load_codes(0);
+      if constexpr (CPF2) {
+#pragma unroll
+        for (int u = 0; u < KS / 4; u += 4) {
+          const uint4 c4 = *reinterpret_cast<const uint4*>(cptr + u);
+          cwn2[u] = c4.x; cwn2[u + 1] = c4.y; cwn2[u + 2] = c4.z; cwn2[u + 3] = c4.w;
+        }
+        load_codes(0);  // cwn = phase 0, cwn2 = phase 1
+      } else if constexpr (!LDSCODE) {
+        load_codes(0);
+      }
       // input: the loader's staging ring (row 0 or the previous workgroup),
       // the wrap row buffer (batch), or the ring of the previous wave
       const int* in_ptr;
@@ -1143,8 +1179,8 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
 #pragma unroll
             for (int v = 0; v < NC; ++v) inv[v] = IN[v][k];
             int cr[3];
-            int ct = gdiag + kp.gap_open * t;
-            if constexpr (swlin(ALG)) asm("" : "+s"(ct));  // one SGPR feeds both the floor and H
+            int ct = pk16(ALG) ? gkp[k] : gdiag + kp.gap_open * t;
+            if constexpr (swlin(ALG) && !pk16(ALG)) asm("" : "+s"(ct));  // one SGPR feeds both the floor and H
             unsigned d;
             if constexpr (ALG == MSA_ALG_NWA && MMODE >= 2) {
               d = step<ALG, OUT, false, TRACKPOS, false>(kp, L, inv, s, t, ct, cr, hv[k]);
@@ -1236,6 +1272,11 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
           for (int h = 0; h < CPP; ++h)
             ntstore(reinterpret_cast<int4*>(a.outDir + obase) + (size_t)(CPP * q + h) * 64 + lane,
                     make_int4((int)dirw[4 * h], (int)dirw[4 * h + 1], (int)dirw[4 * h + 2], (int)dirw[4 * h + 3]));
+        }
+        if constexpr (pk16(ALG)) {
+          // both pairs' H = G - g (i + j): the phase's best of G - g k, minus g (i + j) at its step 0
+          L.best = pk_max(L.best, pk_add(L.pb, pk2(-(gdiag + kp.gap_open * KS * q))));
+          L.pb = (int)0x80008000u;
         }
         MSA_MARK(ph + q, 2);
         // hand the bottom row to the next stripe: lane 63, once per phase

@@ -141,7 +141,7 @@ class Plan:
         lane, items."""
         v = (C.c_int32 * 8)()
         LB.check(LB.lib().msa_plan_launch_info(self._h, v), "msa_plan_launch_info")
-        modes = {0: "stripe", 1: "flow", 2: "chunked", 3: "split", 4: "band", 5: "band_chunked"}
+        modes = {0: "stripe", 1: "flow", 2: "chunked", 3: "split", 4: "band", 5: "band_chunked", 6: "cflow"}
         return dict(mode=modes[v[0]], grid=int(v[1]), threads=int(v[2]), lds_bytes=int(v[3]), nflow=int(v[4]),
                     fill_grid=int(v[5]), rows_per_lane=int(v[6]), items=int(v[7]))
 

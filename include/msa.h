@@ -241,7 +241,8 @@ int msa_plan_results(msa_plan* plan, msa_pair_result* out, void* stream);
 int msa_plan_run_info(msa_plan* plan, int32_t* out4, void* stream);
 /* How the plan launches (for tests and tools): out8 = {mode: 0 stripe_kernel (batch), 1 flow_kernel
  * (single pair, two-pass), 2 chunked banded stripe_kernel, 3 split batch (every pair split into items
- * over several CUs), 4 band_kernel exact chain, 5 band_kernel chunked; workgroups of the main launch;
+ * over several CUs), 4 band_kernel exact chain, 5 band_kernel chunked, 6 cflow_kernel (packed score-only
+ * batch as flag-synchronised chains); workgroups of the main launch;
  * threads per workgroup; dynamic LDS bytes; flow pass-1 workgroups; workgroups of the separate pass-2
  * launch (flow_fill_kernel, long pairs; 0 = pass 2 runs inside the main launch); rows per lane;
  * items}. */
