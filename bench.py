@@ -71,6 +71,8 @@ def parse():
     ap.add_argument("--pairs", type=int, default=0,
                     help="c4: run only the first PAIRS of the 1024 pairs (e.g. 128 = one rank's share at N=8)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c4-strong", action="store_true",
+                    help="c2: skip the same-run C4 strong-scaling sub-record (config.c4_strong)")
     ap.add_argument("--synthetic", action="store_true", help="i.i.d. ACGT (splitmix seed) instead of the dataset")
     return ap.parse_args()
 
@@ -162,6 +164,81 @@ def load_traffic(wl: str, shape: str):
     if d and d.get("hbm_bytes_per_launch"):
         return float(d["hbm_bytes_per_launch"]["total"]), name
     return None, None
+
+
+def c4_strong(rank: int, world: int, dev, steps: int, warmup: int, syn: bool):
+    """The north_star's batch-scaling measurement, taken in the same run as the line's value: C4's fixed
+    1,024 pairs of 4k x 4k (score only) split over the job's ranks (the reference's pair-level fan-out,
+    testing.cpp:112-158 / :269-280), RCCL all-gather of the scores every step, timed between barriers, max
+    over ranks.  Returns the sub-record (rank 0) with GCUPS, ms per step, the all-gather's share and the
+    world size RCCL reports; the scores are checked against the committed fixture."""
+    import torch
+    import torch.distributed as dist
+
+    from cse305_parallel_sequence_alignment_amd import _lib as LB
+    from cse305_parallel_sequence_alignment_amd import data
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+    from cse305_parallel_sequence_alignment_amd.shard import ShardedBatch, broadcast_reference, gather_scores, \
+        shard_range
+
+    total, L = data.C4_PAIRS, data.C4_LEN
+    lo, hi = shard_range(total, rank, world)
+    qs = data.c4_queries(lo, hi, syn)
+    dA = torch.from_numpy(data.encode(b"".join(qs))).to(dev)
+    dB = broadcast_reference(torch.from_numpy(data.encode(data.c4_reference(syn))).to(dev))
+    plan = Plan(LB.SW_LINEAR, LB.CELLS_NONE, [L] * len(qs), [L] * len(qs), [k * L for k in range(len(qs))],
+                [0] * len(qs), match=1, mismatch=0, gap_open=1, gap_extend=1)
+    plan.set_timing(False)
+    local = torch.empty(len(qs), dtype=torch.int32, device=dev)
+
+    def block(lo_, hi_):
+        plan.run(dA, dB)
+        plan.scores_into(local)
+        return local
+
+    batch = ShardedBatch(total, rank, world, block)
+    for _ in range(warmup):
+        batch.step()
+
+    def timed(fn, k):
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = None
+        for _ in range(k):
+            out = fn()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el, out
+
+    el, got = timed(batch.step, steps)
+    gel, _ = timed(lambda: gather_scores(local, total, rank, world), steps)
+    if plan.error():
+        raise SystemExit(f"rank {rank}: c4_strong: a kernel wait hit its spin limit")
+    ok = True
+    fx = REPO / "tests" / "golden" / "c4_scores.json"
+    if not syn and fx.exists():
+        ok = [int(x) for x in got.cpu().tolist()] == json.loads(fx.read_text())["scores"][:total]
+    okt = torch.tensor([int(ok)], dtype=torch.int32, device=dev)
+    if world > 1:
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+    ms = el / steps * 1e3
+    return dict(pairs_total=total, pairs_per_rank=hi - lo, world_size=dist.get_world_size() if world > 1 else 1,
+                value=round(total * L * L / (el / steps) / 1e9, 3), unit="GCUPS", ms_per_step=round(ms, 4),
+                steps=steps, score_allgather_ms=round(gel / steps * 1e3, 4),
+                score_allgather_share=round(gel / el, 4), launch=plan.launch_info()["mode"],
+                scores_match_fixture=bool(okt.item()), scaling="strong",
+                note="C4's 1,024 pairs split over the ranks, measured in this run after the C2 steps; "
+                     "one RCCL all-gather of the scores per step")
 
 
 def launch_ranks(gpus: int) -> int:
@@ -439,6 +516,12 @@ def main():
     if plan.error():
         raise SystemExit(f"rank {rank}: a kernel wait hit its spin limit in the timing pass")
 
+    # the north_star's batch scaling, measured in the same run (C2's value is unchanged by it)
+    strong = c4_strong(rank, world, dev, args.steps, args.warmup, syn) if (wl == "c2" and not args.no_c4_strong) \
+        else None
+    if strong is not None and not strong["scores_match_fixture"]:  # (all-reduced: every rank agrees)
+        raise SystemExit(f"rank {rank}: c4_strong: gathered scores differ from tests/golden/c4_scores.json")
+
     total_cells = cells_per_step * args.steps * world
     gcups = total_cells / elapsed / 1e9
     if rank == 0:
@@ -493,6 +576,7 @@ def main():
                            **({"traceback_ms": round(tb_ms, 4), "traceback_walk": tb_walk} if tb_ms is not None
                               else {}),
                            **({"dp_launch": dp_launch} if dp_launch is not None else {}),
+                           **({"c4_strong": strong} if strong is not None else {}),
                            **({"score_allgather_ms": round(gather_ms, 4),
                                "score_allgather_share": round(gather_ms / (elapsed / args.steps * 1e3), 4)}
                               if gather_ms is not None else {}),

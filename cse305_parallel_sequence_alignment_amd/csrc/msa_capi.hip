@@ -692,7 +692,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   // column, 4 code rings); the column codes stream through fixed-size LDS rings, so any n fits
   const bool aff = kalg == MSA_ALG_SWA || kalg == MSA_ALG_REF1;
   // the code copies: whole rows when they fit (kp.code_whole: no ring bookkeeping), else rings
-  const size_t flow_lds0 = (size_t)(FL_FLAGS + (FL_W + 1) * 256 * (aff ? 2 : 1)) * 4 + ((aff || FL_HO < 2) ? 0 : FL_SINK);
+  const size_t flow_lds0 = (size_t)(FL_FLAGS + (FL_W + 1) * 256 * (aff ? 2 : 1)) * 4;
   const size_t flow_whole = flow_lds0 + (size_t)(aff ? 4 : FL_NCOPY) * (fl_code_bytes((int)desc->n[0]) + 16);
   const bool code_whole = flow_whole <= 96 * 1024;
   const size_t flow_lds = code_whole ? flow_whole : flow_lds0 + (size_t)(aff ? 4 : FL_NCOPY) * FL_CSTR;
@@ -877,7 +877,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
       P->fn = cflow_kernel<CF_W>;
       P->W = CF_W;
       P->KS = 16;
-      P->threads = (CF_W + 2) * 64;
+      P->threads = (CF_W + 1) * 64;
       kp.single = 0;
       kp.lds_code_bytes = L8;
       kp.code_whole = 1;

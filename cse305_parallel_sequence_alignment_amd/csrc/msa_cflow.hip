@@ -27,8 +27,14 @@ namespace msa {
 #ifndef CF_W
 #define CF_W 4    // compute waves (stripes) per item
 #endif
+#ifndef CF_WAITSLEEP
+#define CF_WAITSLEEP 20  // s_sleep (x64 cycles) between the polls of an item still waiting for its first block
+#endif
+#ifndef CF_IOPRIO
+#define CF_IOPRIO 2  // s_setprio of the io wave
+#endif
 #ifndef CF_WPE
-#define CF_WPE 4  // waves per SIMD the register budget is sized for (128 VGPRs): two workgroups of W + 2 waves per CU
+#define CF_WPE 4  // waves per SIMD the register budget is sized for (128 VGPRs): three workgroups of W + 1 waves per CU
 #endif
 
 // Packed profile of one row (pair couple halves separately): score + 2g for codes 0..6, code 7 (the
@@ -61,7 +67,7 @@ __device__ __forceinline__ void cf_profile(int match, int mismatch, int g, unsig
 #endif
 
 template <int W>
-__global__ __launch_bounds__((W + 2) * 64) __attribute__((amdgpu_waves_per_eu(CF_WPE, 8))) void cflow_kernel(KArgs a) {
+__global__ __launch_bounds__((W + 1) * 64) __attribute__((amdgpu_waves_per_eu(CF_WPE, 8))) void cflow_kernel(KArgs a) {
   constexpr int NCP = FL_NCOPY;
   constexpr int PKNEG = (int)0x80008000u;  // -32768 in both halves: "-inf" of a packed value
   extern __shared__ __attribute__((aligned(16))) int smem[];
@@ -78,6 +84,9 @@ __global__ __launch_bounds__((W + 2) * 64) __attribute__((amdgpu_waves_per_eu(CF
   const int g = kp.gap_ext;
   const unsigned ep = kp.epoch;
   const int ncpl = (kp.n_pairs + 1) / 2;  // couples (an odd count repeats its last pair in the high halves)
+  // io-in: the code segment whose whole rows the LDS copies hold (C4's couples share one column
+  // sequence: a workgroup loads it once, not per item -- ~2.5 us of an item's start)
+  long long res_cod = -1;
 
   for (;;) {
     if (threadIdx.x == 0) flags[0] = atomicAdd(a.ticket, 1);
@@ -101,15 +110,25 @@ __global__ __launch_bounds__((W + 2) * 64) __attribute__((amdgpu_waves_per_eu(CF
     const unsigned long long* const g_in = a.gbuf + (size_t)(grp > 0 ? item - ncpl : 0) * a.gbuf_stride;
 
     if (w == W) {
-      // =================== io-in: codes + the row above stripe k0 ===================
+      // =================== io wave ===================
+      // in: codes + the row above stripe k0 (row 0, or item - ncpl's granules) -> link 0's ring
+      // out: the last link's blocks -> granules for item + ncpl.  One wave does both (a workgroup is
+      // W + 1 waves: three fit a CU at 128 VGPRs), issuing a round's granule polls, then copying the
+      // out blocks while the polls fly.
       int* ring = rings;
       int* pub = flags + 32;
       const int* cons = flags + 33;  // compute wave 0's finished phases = blocks it no longer needs
       const int cs_c = fl_cs(k0);
       const int Pc = fl_P(k0, m, n);
       const int Bmax = (k0 == 0) ? Pc - 1 : min(Pc - 1, fl_bmax(k0, m, n));
+      const int kc = k0 + W;  // the next item's first stripe (consumer of the last link)
+      const int bmx = (kc < S) ? fl_bmax(kc, m, n) : -1;
+      const int cs_o = fl_cs(kc);
       const uint8_t* gcod = a.cod + pd.cod_off;
-      int Yr = 0;  // bytes [0, Yr) of every copy's code row are in LDS
+      // bytes [0, Yr) of every copy's code row are in LDS (all of them when the previous item of this
+      // workgroup had the same column segment)
+      int Yr = (pd.cod_off == res_cod) ? L8 : 0;
+      res_cod = pd.cod_off;
       auto load_codes = [&](int Y1) __attribute__((always_inline)) {
         Y1 = min(Y1, L8);
         if (Y1 <= Yr) return;
@@ -132,97 +151,103 @@ __global__ __launch_bounds__((W + 2) * 64) __attribute__((amdgpu_waves_per_eu(CF
         Yr = uni(max(Yr, Y1));
       };
       CF_STAMP(w, 5, __builtin_amdgcn_s_memrealtime());
+      // the hand-offs between items sit on every chain's critical path, and the io wave is the youngest
+      // wave of its SIMD: issue ahead of the chain waves (it mostly polls and sleeps)
+      __builtin_amdgcn_s_setprio(CF_IOPRIO);
       load_codes(1024);
-      int b = 0;
+      int b = 0, bl = 0;
       int consv = 0;
       unsigned spins = 0;
-      while (b <= Bmax) {
-        if (Yr < L8 && Yr < 16 * b + 768) load_codes(Yr + 1024);
-        // up to 16 blocks (256 columns) per round trip: lane l, load r -> block b + 4r + l/16
-        int val[4];
-        int nb = 0;
-        if (k0 == 0) {
+      while (b <= Bmax || bl <= bmx) {
+        bool prog = false;
+        // ---- in: poll the next round's granules (up to 16 blocks; lane l, load r -> block b + 4r + l/16)
+        unsigned long long gv[4];
+        const bool in_act = b <= Bmax;
+        if (in_act) {
+          if (Yr < L8 && Yr < 16 * b + 768) load_codes(Yr + 1024);
+          if (k0 > 0) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) val[r] = pk2(g * (cs_c + 16 * b + 64 * r + lane));  // row 0: H = 0
-          nb = min(16, Bmax - b + 1);
-        } else {
-          unsigned long long gv[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int col = cs_c + 16 * b + 64 * r + lane;
-            gv[r] = gload(g_in + min(max(col + MSA_GOFF, 0), a.gbuf_stride - 1));
-          }
-          bool run = true;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            val[r] = (int)(unsigned)gv[r];
-            const int blk = b + 4 * r + (lane >> 4);
-            const unsigned long long bal = __ballot((blk > Bmax) || ((unsigned)(gv[r] >> 32) == ep));
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-              run = run && (((bal >> (16 * jj)) & 0xffffull) == 0xffffull);
-              if (run) nb = 4 * r + jj + 1;
+            for (int r = 0; r < 4; ++r) {
+              const int col = cs_c + 16 * b + 64 * r + lane;
+              gv[r] = gload(g_in + min(max(col + MSA_GOFF, 0), a.gbuf_stride - 1));
             }
           }
-          nb = uni(min(nb, Bmax - b + 1));
         }
-        // ring slots: block x is free once the consumer has passed x - 16
-        if (consv < b + nb - FL_RINGB) consv = uni(lds_vload(cons));
-        nb = min(nb, consv + FL_RINGB - b);
-        // codes for the blocks' phases must be in LDS before they are published
-        if (Yr < L8 && Yr < 16 * (b + nb) + 192) {
-          load_codes(16 * (b + nb) + 1024);
-          if (Yr < L8) nb = min(nb, (Yr - 192) / 16 - b);
-        }
-        if (nb <= 0) {
-          if (k0 == 0 || consv + FL_RINGB <= b) __builtin_amdgcn_s_sleep(FL_IOSLEEP);  // (granule polls pace themselves)
-          if (++spins > FL_SPIN_MAX) break;
-          continue;
-        }
-        // (every lane stores: blocks past b + nb go to the sink, so no exec-masked branch sits in the
-        // wait loop)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int blk = b + 4 * r + (lane >> 4);
-          int* dst = (blk < b + nb) ? ring + (blk & (FL_RINGB - 1)) * 16 : flags + 96;
-          *L(dst + (lane & 15)) = val[r];
-        }
-        FL_CBAR();
-        if (lane == 0) lds_vstore(pub, b + nb);
-        b += nb;
-      }
-      // (after the loop: a wave-uniform wait loop -- tests/test_host.py::test_wait_loops_are_wave_uniform)
-      if (b <= Bmax && lane == 0) atomicExch(a.err, 20);
-    } else if (w == W + 1) {
-      // =================== io-out: the last link's blocks -> granules for item + ncpl ===================
-      const int kc = k0 + W;  // the next item's first stripe (the link's consumer)
-      if (kc < S) {
-        const int bmx = fl_bmax(kc, m, n);
-        int bl = 0;
-        unsigned spins = 0;
-        while (bl <= bmx) {
+        // ---- out: up to 4 blocks of the last link (while the polls fly)
+        if (bl <= bmx) {
           const int avail = min(uni(lds_vload(flags + 32 + W)) - fl_dq(kc), bmx + 1);
           FL_CBAR();
-          if (avail <= bl) {
-            __builtin_amdgcn_s_sleep(FL_IOSLEEP);
-            if (++spins > FL_SPIN_MAX) break;
-            continue;
-          }
-          const int nb = min(4, avail - bl);
-          const int j = lane >> 4, c = lane & 15;
-          if (j < nb) {
-            const int blk = bl + j;
+          if (avail > bl) {
+            const int nbo = min(4, avail - bl);
+            const int j = lane >> 4, c = lane & 15;
+            const int blk = bl + min(j, nbo - 1);  // (lanes past nbo repeat the last block: no exec branch)
             const int v = *(const lds_int*)(rings + W * 256 + (blk & (FL_RINGB - 1)) * 16 + c);
-            const int col = fl_cs(kc) + 16 * blk + c;
+            const int col = cs_o + 16 * blk + c;
             if (col + MSA_GOFF >= 0 && col + MSA_GOFF < a.gbuf_stride)
               gstore(g_out + col + MSA_GOFF, ((unsigned long long)ep << 32) | (unsigned)v);
+            bl += nbo;
+            FL_CBAR();
+            if (lane == 0) lds_vstore(flags + 64 + W, bl);
+            prog = true;
           }
-          bl += nb;
-          FL_CBAR();
-          if (lane == 0) lds_vstore(flags + 64 + W, bl);
         }
-        if (bl <= bmx && lane == 0) atomicExch(a.err, 21);
+        // ---- in: publish the landed prefix of the round
+        if (in_act) {
+          int val[4];
+          int nb = 0;
+          if (k0 == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) val[r] = pk2(g * (cs_c + 16 * b + 64 * r + lane));  // row 0: H = 0
+            nb = min(16, Bmax - b + 1);
+          } else {
+            bool run = true;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              val[r] = (int)(unsigned)gv[r];
+              const int blk = b + 4 * r + (lane >> 4);
+              const unsigned long long bal = __ballot((blk > Bmax) || ((unsigned)(gv[r] >> 32) == ep));
+#pragma unroll
+              for (int jj = 0; jj < 4; ++jj) {
+                run = run && (((bal >> (16 * jj)) & 0xffffull) == 0xffffull);
+                if (run) nb = 4 * r + jj + 1;
+              }
+            }
+            nb = uni(min(nb, Bmax - b + 1));
+          }
+          // ring slots: block x is free once the consumer has passed x - 16
+          if (consv < b + nb - FL_RINGB) consv = uni(lds_vload(cons));
+          nb = min(nb, consv + FL_RINGB - b);
+          // codes for the blocks' phases must be in LDS before they are published
+          if (Yr < L8 && Yr < 16 * (b + nb) + 192) {
+            load_codes(16 * (b + nb) + 1024);
+            if (Yr < L8) nb = min(nb, (Yr - 192) / 16 - b);
+          }
+          if (nb > 0) {
+            // (every lane stores: blocks past b + nb go to the sink, so no exec-masked branch sits in
+            // the wait loop)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int blk = b + 4 * r + (lane >> 4);
+              int* dst = (blk < b + nb) ? ring + (blk & (FL_RINGB - 1)) * 16 : flags + 96;
+              *L(dst + (lane & 15)) = val[r];
+            }
+            FL_CBAR();
+            if (lane == 0) lds_vstore(pub, b + nb);
+            b += nb;
+            prog = true;
+          }
+        }
+        if (!prog) {
+          // (granule polls pace themselves: the sleep only when nothing was polled this round).  An item
+          // whose producer has not published its first block yet backs off (~0.5 us): hundreds of
+          // waiting items polling back to back load the memory system the running chains hand off through
+          if (in_act && k0 > 0 && b == 0) __builtin_amdgcn_s_sleep(CF_WAITSLEEP);
+          else if (!in_act || k0 == 0 || consv + FL_RINGB <= b) __builtin_amdgcn_s_sleep(FL_IOSLEEP);
+          if (++spins > FL_SPIN_MAX) break;
+        }
       }
+      // (after the loop: a wave-uniform wait loop -- tests/test_host.py::test_wait_loops_are_wave_uniform)
+      if ((b <= Bmax || bl <= bmx) && lane == 0) atomicExch(a.err, 20);
     } else if (k0 + w < S) {
       // =================== compute wave: stripe k of the couple ===================
       const int k = k0 + w;
@@ -255,20 +280,16 @@ __global__ __launch_bounds__((W + 2) * 64) __attribute__((amdgpu_waves_per_eu(CF
       // H = G - g(i+j), i+j = 64k + 1 + cs + t for every lane of step t: per step the phase's best of
       // G - g kx (gk: SGPR constants), per phase minus g(i+j) at its step 0
       const int negct0 = -g * (64 * k + 1 + cs);
-      int gk[16];
+      int gk[16];  // pk2(-g k); only k = 1, 2, 4, 8 are used (the tree's level offsets)
 #pragma unroll
       for (int kx = 0; kx < 16; ++kx) {
         gk[kx] = pk2(-g * kx);
-#ifdef CF_GKV
-        asm("" : "+v"(gk[kx]));
-#else
-        asm("" : "+s"(gk[kx]));
-#endif
+        if (kx == 1 || kx == 2 || kx == 4 || kx == 8) asm("" : "+s"(gk[kx]));
       }
       // left neighbour and diagonal at step 0: virtual cells, H = 0 (G = g(i+j))
       int X = pk2(g * (64 * k + cs));
       int U = pk2(g * (64 * k + cs - 1));
-      int best = 0, pb = PKNEG;
+      int best = 0;
       int pubv = 0, consv = 0;
       unsigned spins = 0;
       bool stuck = false;
@@ -369,16 +390,30 @@ __global__ __launch_bounds__((W + 2) * 64) __attribute__((amdgpu_waves_per_eu(CF
             if (kx == FL_PF) issue_reads(q + 1, INn, CWn, pubn);  // prefetch phase q+1 (6 DS ops)
             // both pairs' score + 2g as int16: {s4 byte kk, 0, s4b byte kk, 0}
             const int s = (int)__builtin_amdgcn_perm(s4b, s4, 0x0c000c00u | ((4u + kk) << 16) | (unsigned)kk);
-            const int up = dpp_shr1(IN[u][kk], X);
-            const int h = pk_max(pk_max(pk_add(U, s), X), up);
+            // diagonal and left first (no wait on this step's DPP), then the cell above: the DPP reads X
+            // three instructions after the previous step wrote it (its two wait states, no s_nop), and
+            // writes in place into the input register, whose lane 0 holds the row above (no copy)
+            const int dl = pk_max(pk_add(U, s), X);
+            int up = IN[u][kk];
+            asm volatile("v_mov_b32_dpp %0, %1 wave_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(up) : "v"(X));
+            X = pk_max(dl, up);
             U = up;
-            X = h;
-            xo[kx] = h;
-            pb = pk_max(pb, pk_add(h, gk[kx]));
+            xo[kx] = X;
           }
         }
-        best = pk_max(best, pk_add(pb, pk2(negct0 - 16 * g * q)));
-        pb = PKNEG;
+        // the phase's best of both pairs' H: max over k of G_k - g k as a tree (four levels of
+        // independent ops, no serial chain), minus g(i+j) at step 0
+        {
+          int r8[8], r4[4], r2[2];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) r8[j] = pk_max(xo[2 * j], pk_add(xo[2 * j + 1], gk[1]));
+#pragma unroll
+          for (int j = 0; j < 4; ++j) r4[j] = pk_max(r8[2 * j], pk_add(r8[2 * j + 1], gk[2]));
+#pragma unroll
+          for (int j = 0; j < 2; ++j) r2[j] = pk_max(r4[2 * j], pk_add(r4[2 * j + 1], gk[4]));
+          const int r1 = pk_max(r2[0], pk_add(r2[1], gk[8]));
+          best = pk_max(best, pk_add(r1, pk2(negct0 - 16 * g * q)));
+        }
         lgkm_wait<5>(pubn);  // the counter read (oldest of the six) has landed
         pubv = uni(pubn);
         // hand-off: lane 63's 16 values of this phase = block q - dq of the out ring

@@ -47,7 +47,6 @@ namespace msa {
 #define FL_OFF 95       // LDS code copy x, byte y <-> column y + x - FL_OFF (== CPAD-1 mod 16)
 #define FL_NCOPY 8      // byte-shifted LDS code copies (8-byte aligned 8-code reads)
 #define FL_FLAGS 128    // ints of flags at the start of LDS
-#define FL_SINK 1152    // bytes of the SW-linear hand-off sink after the code copies (FL_HO 2)
 // Column codes stream through an LDS ring per copy: copy-local byte y sits at y mod FL_CRING,
 // and the 16 bytes at ring position 0 are mirrored past the end (FL_CSTR = ring + guard), so
 // every 16-byte read at any ring position is contiguous.  io-in refills a slot once every
@@ -69,16 +68,6 @@ namespace msa {
 #endif
 #ifndef FL_FSLEEP
 #define FL_FSLEEP 32    // s_sleep between a pass-2 wave's polls of its block's last granule
-#endif
-#ifndef FL_PUBLATE
-#define FL_PUBLATE 0    // 1: the producer-counter read is awaited after the hand-off, with the data
-#endif
-#ifndef FL_HO
-#define FL_HO 0         // SW-linear hand-off: 0 = 16 ds_write_addtid_b32, 1 = 8 ds_write_b64 (both lane 63
-                        // alone), 2 = 4 ds_write_b128 of every lane (lanes 0..62 into a sink; measured
-                        // C2 0.478 vs 0.455 ms: the 1 KiB writes cost more LDS time than the exec switch),
-                        // 3 = a DPP shift register (one wave_shl:1 per step collects lane 63's values in
-                        // lanes 48..63) and two every-lane ds_write_b32 (lanes 0..47 into the sink)
 #endif
 #ifndef FL_IOSLEEP
 #define FL_IOSLEEP 1    // s_sleep of an idle io wave
@@ -194,52 +183,8 @@ __device__ __forceinline__ void ds_handoff_tid(unsigned long long m63, unsigned 
       : "memory");
 }
 
-// The same hand-off as 8 single-lane ds_write_b64 + the counter (9 DS ops instead of 17: with
-// the phase's 6 prefetch reads in flight, 23 outstanding DS ops exceed the 15 lgkmcnt tracks)
-typedef int fl_v2i __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void ds_handoff_b64(unsigned long long m63, unsigned addr, const int (&x)[16], unsigned pa,
-                                               int pv) {
-  unsigned long long sv;
-  const fl_v2i x0{x[0], x[1]}, x1{x[2], x[3]}, x2{x[4], x[5]}, x3{x[6], x[7]};
-  const fl_v2i x4{x[8], x[9]}, x5{x[10], x[11]}, x6{x[12], x[13]}, x7{x[14], x[15]};
-  asm volatile(
-      "s_mov_b64 %[sv], exec\n\ts_mov_b64 exec, %[m]\n\t"
-      "ds_write_b64 %[a], %[x0] offset:0\n\tds_write_b64 %[a], %[x1] offset:8\n\t"
-      "ds_write_b64 %[a], %[x2] offset:16\n\tds_write_b64 %[a], %[x3] offset:24\n\t"
-      "ds_write_b64 %[a], %[x4] offset:32\n\tds_write_b64 %[a], %[x5] offset:40\n\t"
-      "ds_write_b64 %[a], %[x6] offset:48\n\tds_write_b64 %[a], %[x7] offset:56\n\t"
-      "ds_write_b32 %[pa], %[pv]\n\t"
-      "s_mov_b64 exec, %[sv]\n\ts_nop 4"
-      : [sv] "=&s"(sv)
-      : [m] "s"(m63), [a] "v"(addr), [x0] "v"(x0), [x1] "v"(x1), [x2] "v"(x2), [x3] "v"(x3), [x4] "v"(x4),
-        [x5] "v"(x5), [x6] "v"(x6), [x7] "v"(x7), [pa] "v"(pa), [pv] "v"(pv)
-      : "memory");
-}
 
-// The same hand-off with every lane active: no exec switch, so no SALU exec writes and no
-// wait states before the next DPP.  Lane 63 writes its 16 values as four b128 to the ring
-// block (wa) and the counter (pa); lanes 0..62 write the same-shaped data to the shared sink
-// (wa = sink + 16 lane, pa = sink + 4 lane: consecutive lanes, no bank conflicts), which
-// nothing reads.  5 DS ops instead of 17.
-__device__ __forceinline__ void ds_handoff_all(unsigned wa, const fl_v4i (&x)[4], unsigned pa, int pv) {
-  asm volatile(
-      "ds_write_b128 %[a], %[x0]\n\tds_write_b128 %[a], %[x1] offset:16\n\t"
-      "ds_write_b128 %[a], %[x2] offset:32\n\tds_write_b128 %[a], %[x3] offset:48\n\t"
-      "ds_write_b32 %[pa], %[pv]"
-      :
-      : [a] "v"(wa), [x0] "v"(x[0]), [x1] "v"(x[1]), [x2] "v"(x[2]), [x3] "v"(x[3]), [pa] "v"(pa), [pv] "v"(pv)
-      : "memory");
-}
 
-// FL_HO 3: lanes 48..63 hold lane 63's 16 values of the phase (the shift register); every lane
-// writes one dword -- lanes 48..63 to the ring block, the others to the sink -- then the counter
-// (lane 63 to its flag, the others to the sink).  2 DS ops, no exec switch, no wait states.
-__device__ __forceinline__ void ds_handoff_sh(unsigned wa, int x, unsigned pa, int pv) {
-  asm volatile("ds_write_b32 %[a], %[x]\n\tds_write_b32 %[pa], %[pv]"
-               :
-               : [a] "v"(wa), [x] "v"(x), [pa] "v"(pa), [pv] "v"(pv)
-               : "memory");
-}
 
 // Affine hand-off: lane 63 alone writes its 16 Z and 16 F~ of the phase as 8 b128 writes
 // (the F~ half of a link's ring sits 1 KiB after the Z half), then the phase counter.
@@ -394,13 +339,8 @@ struct FillArgs {
 // setup and every access a private-memory load).
 typedef const __attribute__((address_space(4))) struct KArgs kargs_c;
 __device__ __forceinline__ FillArgs fill_args_of(kargs_c* k) {
-#ifdef FL_KA_UNI
-  // (measured: the pointer made wave-uniform -- scalar loads of the arguments instead of vector
-  // loads -- made C2 slower, 0.466 -> 0.476 ms; off)
-  const unsigned long long kv = (unsigned long long)k;
-  k = (kargs_c*)(((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(kv >> 32)) << 32) |
-                 (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)kv));
-#endif
+  // (measured: the pointer made wave-uniform -- scalar loads of the arguments instead of vector loads --
+  // made C2 slower, 0.466 -> 0.476 ms)
   const msa_pair_desc pd = k->pairs[0];
   return FillArgs{k->A, k->cod, k->br, k->snap, k->outH, k->blk, k->err, k->cod_copy, pd.a_off, pd.cod_off,
                   pd.out_off, pd.m, pd.n, pd.pmax, k->nseg, k->brw, k->kp.match, k->kp.mismatch, k->kp.gap_ext,
@@ -411,16 +351,8 @@ __device__ __forceinline__ FillArgs fill_args_of(kargs_c* k) {
   };
 }
 template <bool FLOOR, bool TRACKPOS, int R>
-#ifndef FL_FB_PTR
-#define FL_FB_VAL  // SW-linear pass-2 blocks take their arguments by value (C2 0.4646 -> 0.4604 ms against the kernarg pointer)
-#endif
-#ifdef FL_FB_VAL
+// SW-linear pass-2 blocks take their arguments by value (C2 0.4646 -> 0.4604 ms against the kernarg pointer)
 __device__ __attribute__((noinline)) void fill_block(const FillArgs fa, int blk, int lane, lds_int* lds);
-#define FL_FB_ARG(ka_) fill_args_of(ka_)
-#else
-__device__ __attribute__((noinline)) void fill_block(kargs_c* ka, int blk, int lane, lds_int* lds);
-#define FL_FB_ARG(ka_) (ka_)
-#endif
 __device__ __attribute__((noinline)) void fill_block_aff(kargs_c* ka, int blk, int lane, lds_int* lds);
 __device__ __attribute__((noinline)) void fill_block_aff2(kargs_c* ka, int blk, int lane, lds_int* lds);
 __device__ __attribute__((noinline)) void fill_block_got(kargs_c* ka, int blk, int lane, lds_int* lds);
@@ -482,11 +414,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
   // except that the first 8 arrivals take chunk = arrival: every chunk's first item is then
   // claimed by a running workgroup even if the workgroup with blockIdx c is not resident (CUs
   // held by other launches), and a chunk's later items wait only on claimed ones.
-#ifdef FL_GRP_BLK
-  const int grp = (int)(blockIdx.x & 7);  // (diagnostic: round 3's choice)
-#else
-  const int grp = arrival < 8 ? arrival : (int)(blockIdx.x & 7);
-#endif
+  const int grp = arrival < 8 ? arrival : (int)(blockIdx.x & 7);  // (blockIdx & 7 alone: C2 0.539 vs 0.459 ms)
   if constexpr (SAVE) {
 #ifdef MSA_STAMPS
     if (a.stamps && threadIdx.x == 0 && blockIdx.x < 2048)
@@ -511,7 +439,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
         else if constexpr (GOT) fill_block_got(ka, a.border[t], lane, wl);
         else if constexpr (AFF && R == 2) fill_block_aff2(ka, a.border[t], lane, wl);
         else if constexpr (AFF) fill_block_aff(ka, a.border[t], lane, wl);
-        else fill_block<FLOOR, TRACKPOS, R>(FL_FB_ARG(ka), a.border[t], lane, wl);
+        else fill_block<FLOOR, TRACKPOS, R>(fill_args_of(ka), a.border[t], lane, wl);
       }
 #ifdef MSA_STAMPS
       wg_stamp(1, __builtin_amdgcn_s_memrealtime());
@@ -1133,19 +1061,6 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
       const unsigned a_cons2 = lds_addr(flags + 64 + w + 1);
       const bool two_cons = SAVE || (w + 1 == W);
       const unsigned a_dummy = lds_addr(flags + 96 + 8 * (w & 1));  // sink for a phase with nothing to hand off
-#if FL_HO == 2
-      // every-lane hand-off: lanes 0..62 (and lane 63 with nothing to hand off) write to the
-      // sink after the code copies (FL_SINK bytes, shared by the compute waves, never read)
-      const unsigned a_sink = lds_addr(codes + FL_NCOPY * cstr) + 16u * (unsigned)lane;
-      const unsigned a_pa = (lane == 63) ? a_prog_me : lds_addr(codes + FL_NCOPY * cstr) + 4u * (unsigned)lane;
-#elif FL_HO == 3
-      // shift-register hand-off: lanes 48..63 write the ring block (wa + 4 (lane - 48)), the others the
-      // sink after the code copies (shared by the compute waves, never read); the counter likewise
-      const unsigned a_sink = lds_addr(codes + FL_NCOPY * cstr) + 4u * (unsigned)lane;
-      const unsigned a_pa = (lane == 63) ? a_prog_me : a_sink + 256u;
-      const bool sh_lane = lane >= 48;
-      int shreg = 0;
-#endif
       unsigned plo, phi, plo2 = 0, phi2 = 0;
       fl_profile<GS, FLOOR>(kp.match, kp.mismatch, g, ac, plo, phi);
       if constexpr (R == 2) fl_profile<GS, FLOOR>(kp.match, kp.mismatch, g, ac2, plo2, phi2);
@@ -1279,18 +1194,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
           }
         }
         int hv[16];
-#if FL_HO == 2
-        fl_v4i xo4[4];
-#define FL_XO(kx_) xo4[(kx_) >> 2][(kx_) & 3]
-#elif FL_HO == 3
-#define FL_PUT(kx_, v_) (shreg = dpp_shl1((v_), shreg))
-#else
-        int xo[16];
-#define FL_XO(kx_) xo[kx_]
-#endif
-#ifndef FL_PUT
-#define FL_PUT(kx_, v_) (FL_XO(kx_) = (v_))
-#endif
+        int xo[16];  // lane 63's values of the phase are the hand-off
         int pubn = 0;
         const int negct = negct0 - 16 * g * q;
 #pragma unroll
@@ -1304,7 +1208,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
             const int s = ((int)(s4 << (24 - 8 * kk))) >> 24;
             if constexpr (R == 1) {
               const int h = fl_step<GS, FLOOR>(IN[kx >> 2][kx & 3], s, X, U, g);
-              FL_PUT(kx, X);
+              xo[kx] = X;
               if constexpr (BEST) hv[kx] = GS ? h + negct + gk[kx] : h;
             } else {
               // row 1's up = the previous lane's row 2 (lane 0: the producer's value);
@@ -1321,7 +1225,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
               if constexpr (FLOOR) h2 = imax(h2, 0);
               asm("" : "+v"(h2));
               X2 = GS ? h2 : h2 - g;
-              FL_PUT(kx, X2);
+              xo[kx] = X2;
             }
           }
         }
@@ -1329,35 +1233,22 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
           for (int kx = 0; kx < 16; kx += 2) best = imax3(best, hv[kx], hv[kx + 1]);
         }
-#if !FL_PUBLATE
         lgkm_wait<5>(pubn);  // the counter read (oldest of the six) has landed
         pubv = uni(pubn);
-#endif
         // hand-off: lane 63's 16 values of this phase = block q - dq of the out ring
         const int bq = q - dq;
         const bool wr = has_out && bq >= 0;
         if (__builtin_expect((MSA_ABL & 80) == 0 && wr && consv < bq - (FL_RINGB - 1), 0))
           refresh_cons(bq - (FL_RINGB - 1));
         const unsigned wa = wr ? a_ring_out + (unsigned)((bq & (FL_RINGB - 1)) * 64) : a_dummy;
-#if FL_HO == 2
-        ds_handoff_all((lane == 63 && wr) ? wa : a_sink, xo4, a_pa, q + 1);
-#elif FL_HO == 3
-        ds_handoff_sh((sh_lane && wr) ? wa - 192u + 4u * (unsigned)lane : a_sink, shreg, a_pa, q + 1);
-#elif FL_HO == 1
-        ds_handoff_b64(m63, wa, xo, a_prog_me, q + 1);
-#else
-        ds_handoff_tid(m63, wa - 252u, xo, a_prog_me, q + 1);  // (-6.5% on C2 vs four single-lane b128 writes)
-#endif
-#undef FL_XO
-#undef FL_PUT
+        // lane 63 alone: 16 ds_write_addtid_b32 + the counter (measured 6.5% faster on C2 than four
+        // single-lane b128 writes; 8 b64 writes, every-lane b128 writes into a sink and a DPP shift
+        // register were slower -- DESIGN.md section 5)
+        ds_handoff_tid(m63, wa - 252u, xo, a_prog_me, q + 1);
 #ifdef MSA_STAMPS
         if (q == dq) FL_STAMP(0, 3, __builtin_amdgcn_s_memrealtime());
 #endif
         lgkm_wait_v<5>(INn, CWn);  // phase q+1's prefetched inputs have landed (the writes may fly)
-#if FL_PUBLATE
-        lgkm_wait<5>(pubn);  // (landed with them: it was read first)
-        pubv = uni(pubn);
-#endif
         if constexpr (MASK) mask_in(q + 1, INn);
       };
       using T_ = std::true_type;
@@ -1459,12 +1350,7 @@ __device__ __forceinline__ fl_v4u p2_codes(lds_int* lds, int k, int lane) {
 // R = 2: lane r holds rows 128s+2r+1 (X/U) and 128s+2r+2 (X2); cells go to the
 // R = 2 layout (per 4 steps: the wave's row-1 int4s, then its row-2 int4s).
 template <bool FLOOR, bool TRACKPOS, int R>
-#ifdef FL_FB_VAL
 __device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, int lane, lds_int* lds) {
-#else
-__device__ __attribute__((noinline)) void fill_block(kargs_c* ka, int blk, int lane, lds_int* lds) {
-  const FillArgs a = fill_args_of(ka);
-#endif
   constexpr bool GS = !FLOOR;
   const unsigned ep = a.ep;
   const int m = a.m, n = a.n, S = (m + 64 * R - 1) / (64 * R), g = a.g;
@@ -1626,11 +1512,7 @@ __device__ __attribute__((noinline)) void fill_block_aff(kargs_c* ka, int blk, i
   const int m = a.m, n = a.n, S = (m + 63) / 64, g = a.g, oe = a.oe;
   const int s = blk / a.nseg, seg = blk - s * a.nseg;
   int bb = INT32_MIN, bi = 0, bj = 0;
-#ifdef MSA_AFF_NOP2
-  if (false) {  // timing variant: pass 1 alone
-#else
   if (s < S) {
-#endif
     const int P = fl_P(s, m, n, 1);
     const int q0 = seg * FL_PS;
     if (q0 < P) {
@@ -2255,7 +2137,7 @@ __global__ __launch_bounds__(FL_FILLW * 64) __attribute__((amdgpu_waves_per_eu(F
     else if constexpr (FK == 2) fill_block_got(ka, a.border[t], lane, wl);
     else if constexpr (FK == 1 && R == 2) fill_block_aff2(ka, a.border[t], lane, wl);
     else if constexpr (FK == 1) fill_block_aff(ka, a.border[t], lane, wl);
-    else fill_block<FLOOR, TRACKPOS, R>(FL_FB_ARG(ka), a.border[t], lane, wl);
+    else fill_block<FLOOR, TRACKPOS, R>(fill_args_of(ka), a.border[t], lane, wl);
   }
 }
 

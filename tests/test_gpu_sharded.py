@@ -62,7 +62,12 @@ def _worker(rank, world, port, q):
 
             batch = ShardedBatch(total, rank, world, score_block)
             got = [batch.step().cpu().tolist() for _ in range(2)]
-            q.put((rank, dict(scores=got, err=plan.error(), n=hi - lo)))
+            # bench.py's same-run strong-scaling record (config.c4_strong): the same split, timed between
+            # barriers, max over ranks, scores checked against the fixture
+            import bench
+
+            strong = bench.c4_strong(rank, world, dev, 2, 1, False)
+            q.put((rank, dict(scores=got, err=plan.error(), n=hi - lo, strong=strong)))
         finally:
             dist.destroy_process_group()
     except Exception:
@@ -91,3 +96,6 @@ def test_c4_sharded_device_world2(dev):
         assert out[r]["n"] == 512
         for step in out[r]["scores"]:
             assert step == want
+        st = out[r]["strong"]
+        assert st["scores_match_fixture"] and st["pairs_per_rank"] == 512 and st["world_size"] == 2
+        assert st["pairs_total"] == 1024 and st["value"] > 0 and 0 <= st["score_allgather_share"] <= 1
