@@ -858,8 +858,8 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     }
   }
   // Packed score-only batches (C4): cflow_kernel (msa_cflow.hip) -- items of CF_W stripes of one couple,
-  // chained through granules, claimed item-major -- when the couples' code rows fit LDS.  MSA_C4_KERNEL=
-  // lockstep (diagnostic) keeps stripe_kernel's lock-step batch / split modes.
+  // chained through granules, claimed item-major -- for batches of fewer couples than two per CU whose code
+  // rows fit LDS.  MSA_C4_KERNEL=lockstep / =cflow (diagnostics) force either kernel.
   if (kalg == MSA_ALG_SWLP && !single) {
     static const bool lockstep = [] {
       const char* e = std::getenv("MSA_C4_KERNEL");
@@ -872,7 +872,15 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     }
     const int L8 = fl_code_bytes((int)nmax);
     const size_t clds = (size_t)(FL_FLAGS + (CF_W + 1) * 256) * 4 + (size_t)FL_NCOPY * (L8 + 16);
-    if (!lockstep && clds <= 96 * 1024) {
+    // a batch with at least two couples per CU keeps the lock-step kernel's SIMDs busy (its 8 waves per
+    // workgroup hide each other's step latency): measured on C4's shape, 1,024 pairs 2.39 ms lock-step vs
+    // 2.73 cflow; 512 pairs 2.07 vs 1.58, 128 pairs 0.72 vs 0.55 (profiles/r05_c4_*_bench.json)
+    const int ncpl = (int)((desc->n_pairs + 1) / 2);
+    static const bool force_cflow = [] {
+      const char* e = std::getenv("MSA_C4_KERNEL");
+      return e && std::strcmp(e, "cflow") == 0;
+    }();
+    if (!lockstep && clds <= 96 * 1024 && (force_cflow || ncpl < 2 * device_cus())) {
       P->cflow = true;
       P->fn = cflow_kernel<CF_W>;
       P->W = CF_W;
@@ -881,7 +889,6 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
       kp.single = 0;
       kp.lds_code_bytes = L8;
       kp.code_whole = 1;
-      const int ncpl = (int)((desc->n_pairs + 1) / 2);
       const int G = (int)(((mmax + 63) / 64 + CF_W - 1) / CF_W);
       kp.n_items = ncpl * G;
       kp.sched_cap = 0;
