@@ -27,18 +27,6 @@ namespace msa {
 #ifndef CF_W
 #define CF_W 4    // compute waves (stripes) per item
 #endif
-#ifndef CF_WAITSLEEP
-#define CF_WAITSLEEP 20  // s_sleep (x64 cycles) between the polls of an item still waiting for its first block
-#endif
-#ifndef CF_DIRECT
-#define CF_DIRECT 0  // 1: an item's first compute wave reads the previous item's granules itself (CF_D phases ahead)
-#endif
-#ifndef CF_D
-#define CF_D 3
-#endif
-#ifndef CF_IOPRIO
-#define CF_IOPRIO 2  // s_setprio of the io wave
-#endif
 #ifndef CF_WPE
 #define CF_WPE 4  // waves per SIMD the register budget is sized for (128 VGPRs): three workgroups of W + 1 waves per CU
 #endif
@@ -157,19 +145,8 @@ __global__ __launch_bounds__((W + 1) * 64) __attribute__((amdgpu_waves_per_eu(CF
         Yr = uni(max(Yr, Y1));
       };
       CF_STAMP(w, 5, __builtin_amdgcn_s_memrealtime());
-      // the hand-offs between items sit on every chain's critical path, and the io wave is the youngest
-      // wave of its SIMD: issue ahead of the chain waves (it mostly polls and sleeps)
-      __builtin_amdgcn_s_setprio(CF_IOPRIO);
       int b = 0, bl = 0;
-      if (CF_DIRECT && k0 > 0) {
-        // compute wave 0 reads the previous item's granules itself: every code first, then the flag
-        load_codes(L8);
-        FL_CBAR();
-        if (lane == 0) lds_vstore(flags + 34, 1);
-        b = Bmax + 1;
-      } else {
-        load_codes(1024);
-      }
+      load_codes(1024);
       int consv = 0;
       unsigned spins = 0;
       while (b <= Bmax || bl <= bmx) {
@@ -252,11 +229,8 @@ __global__ __launch_bounds__((W + 1) * 64) __attribute__((amdgpu_waves_per_eu(CF
           }
         }
         if (!prog) {
-          // (granule polls pace themselves: the sleep only when nothing was polled this round).  An item
-          // whose producer has not published its first block yet backs off (~0.5 us): hundreds of
-          // waiting items polling back to back load the memory system the running chains hand off through
-          if (in_act && k0 > 0 && b == 0) __builtin_amdgcn_s_sleep(CF_WAITSLEEP);
-          else if (!in_act || k0 == 0 || consv + FL_RINGB <= b) __builtin_amdgcn_s_sleep(FL_IOSLEEP);
+          // (granule polls pace themselves: the sleep only when nothing was polled this round)
+          if (!in_act || k0 == 0 || consv + FL_RINGB <= b) __builtin_amdgcn_s_sleep(FL_IOSLEEP);
           if (++spins > FL_SPIN_MAX) break;
         }
       }
@@ -368,45 +342,7 @@ __global__ __launch_bounds__((W + 1) * 64) __attribute__((amdgpu_waves_per_eu(CF
           for (int u = 0; u < 4; ++u) IN[u] = fl_v4i{PKNEG, PKNEG, PKNEG, PKNEG};
         }
       };
-      // CF_DIRECT: wave 0 of an item after the first loads the previous item's {epoch, value} granules of
-      // block b (lanes 0..15: its 16 columns) CF_D phases ahead and writes the landed values into its own
-      // input ring (the slot it reads at phase b - 1's step FL_PF): no io wave between the two chains
-      const bool din = CF_DIRECT && w == 0 && k0 > 0;
-      unsigned long long gpre[CF_D];
-      const int* dring = rings;  // (wave 0's input ring = link 0)
-      auto dload = [&](int blk) __attribute__((always_inline)) {
-        const int col = cs + 16 * blk + (lane & 15);
-        return gload(g_in + min(max(col + MSA_GOFF, 0), a.gbuf_stride - 1));
-      };
-      auto dput = [&](int blk, unsigned long long gv) __attribute__((always_inline)) {
-        if (blk > Bin) return;  // (masked by mask_in)
-        bool ok = __ballot(lane >= 16 || (unsigned)(gv >> 32) == ep) == ~0ull;
-        unsigned sp = 0;
-        while (!ok) {
-          __builtin_amdgcn_s_sleep(1);
-          gv = dload(blk);
-          ok = __ballot(lane >= 16 || (unsigned)(gv >> 32) == ep) == ~0ull;
-          if (++sp > FL_SPIN_MAX) break;
-        }
-        stuck = stuck || !ok;
-        *L(const_cast<int*>(dring) + (blk & (FL_RINGB - 1)) * 16 + (lane & 15)) = (int)(unsigned)gv;
-      };
-      if (din) {
-        int cr = 0;
-        while (cr == 0) {  // the io wave has every code in LDS
-          cr = uni(lds_vload(flags + 34));
-          if (cr == 0) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > FL_SPIN_MAX) { stuck = true; break; }
-          }
-        }
-        dput(0, dload(0));
-#pragma unroll
-        for (int d = 0; d < CF_D; ++d) gpre[d] = dload(1 + d);
-        pubv = 1 << 29;  // (its input counter is never read)
-      } else {
-        wait_flag(a_prog_in, pubv, min(1, Bin + 1) + dq_in);
-      }
+      wait_flag(a_prog_in, pubv, min(1, Bin + 1) + dq_in);
       {
         int pub0;
         issue_reads(0, INa, CWa, pub0);
@@ -429,13 +365,6 @@ __global__ __launch_bounds__((W + 1) * 64) __attribute__((amdgpu_waves_per_eu(CF
           wait_flag(a_prog_in, pubv, need + dq_in);
           reread_in(q, IN);
           if constexpr (MASK) mask_in(q, IN);
-        }
-        if (CF_DIRECT && din) {
-          // block q + 1 (read at this phase's step FL_PF) into the ring; prefetch block q + 1 + CF_D
-          dput(q + 1, gpre[0]);
-#pragma unroll
-          for (int d = 0; d + 1 < CF_D; ++d) gpre[d] = gpre[d + 1];
-          gpre[CF_D - 1] = dload(q + 1 + CF_D);
         }
         int xo[16];
         int pubn = 0;

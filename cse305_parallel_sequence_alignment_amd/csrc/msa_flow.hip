@@ -78,6 +78,17 @@ namespace msa {
 #ifndef MSA_ABL
 #define MSA_ABL 0
 #endif
+// Gotoh pass 1 (R = 2): row 1 computes on tag-carrying values except at a phase's last step
+#ifndef FL_GOT_UNTAG
+#define FL_GOT_UNTAG 1
+#endif
+// v_max3_i32 as one opaque instruction: the compiler re-associates three max3 that share an operand
+// (h, R~, D~ of one cell) into a max + two max + a max3 -- four VALU instead of three
+__device__ __forceinline__ int vmax3(int a, int b, int c) {
+  int d;
+  asm("v_max3_i32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
 
 __host__ __device__ __forceinline__ int fl_cs(int k) { return -((16 - (k & 15)) & 15); }  // -((-k) mod 16)
 // R rows per lane: stripe k holds rows 64Rk+1 .. 64R(k+1); rlast = last lane with a row
@@ -855,13 +866,27 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
               // row 1: the cell above is the previous lane's row 2 (lane 0: the link)
               const int uH = dpp_shr1(Z[kx >> 2][kx & 3], Zl2);
               const int uD = dpp_shr1(F[kx >> 2][kx & 3], Fo2);
-              const int t1 = (int)((unsigned)U | 3u) + sc;
-              const int t2p = (int)(((unsigned)E & ~3u) | 2u);
-              const int t3p = (int)(((unsigned)uD & ~3u) | 1u);
-              const int t2 = t2p - 4 * oe, t3 = t3p - 4 * oe;
-              int h1 = imax3(t1, t2, t3);
-              int rr1 = imax3(t1, t2p, t3);
-              int dd1 = imax3(t1, t2, t3p);
+              int h1, rr1, dd1;
+              if (kx == 15 || !FL_GOT_UNTAG) {
+                const int t1 = (int)((unsigned)U | 3u) + sc;
+                const int t2p = (int)(((unsigned)E & ~3u) | 2u);
+                const int t3p = (int)(((unsigned)uD & ~3u) | 1u);
+                const int t2 = t2p - 4 * oe, t3 = t3p - 4 * oe;
+                h1 = vmax3(t1, t2, t3);
+                rr1 = vmax3(t1, t2p, t3);
+                dd1 = vmax3(t1, t2, t3p);
+              } else {
+                // Pass 1 never reads a tag: every consumer of a cell re-tags it (t1 = (U | 3) + s, the
+                // and-or of t2p / t3p), so row 1's candidates keep their inputs' tag bits (values are
+                // 4v + tag, tag in 1..3: the maxima and every value are exact).  Row 1's tags are only
+                // exported through SNAP, i.e. by a phase's last step (kx 15, tagged above); row 2 feeds
+                // the hand-off (BR) at every step and stays tagged.  3 VALU per step fewer.
+                const int t1 = U + sc;
+                const int t2 = E - 4 * oe, t3 = uD - 4 * oe;
+                h1 = vmax3(t1, t2, t3);
+                rr1 = vmax3(t1, E, t3);
+                dd1 = vmax3(t1, t2, uD);
+              }
               asm("" : "+v"(h1));
               // row 2: diagonal = row 1's previous H~, above = row 1's new cell
               const int sb = ((int)(s4b << (24 - 8 * kk))) >> 24;
@@ -875,17 +900,17 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
                 rr1 = before ? 1 - 4 * oe : rr1;
                 dd1 = before ? 1 : dd1;
                 const int s3p = (int)(((unsigned)dd1 & ~3u) | 1u), s3 = s3p - 4 * oe;
-                h2 = imax3(s1, s2, s3);
-                rr2 = imax3(s1, s2p, s3);
-                dd2 = imax3(s1, s2, s3p);
+                h2 = vmax3(s1, s2, s3);
+                rr2 = vmax3(s1, s2p, s3);
+                dd2 = vmax3(s1, s2, s3p);
                 h2 = before ? 1 - 4 * oe : h2;
                 rr2 = before ? 1 - 4 * oe : rr2;
                 dd2 = before ? 1 : dd2;
               } else {
                 const int s3p = (int)(((unsigned)dd1 & ~3u) | 1u), s3 = s3p - 4 * oe;
-                h2 = imax3(s1, s2, s3);
-                rr2 = imax3(s1, s2p, s3);
-                dd2 = imax3(s1, s2, s3p);
+                h2 = vmax3(s1, s2, s3);
+                rr2 = vmax3(s1, s2p, s3);
+                dd2 = vmax3(s1, s2, s3p);
               }
               asm("" : "+v"(h2));
               U = uH;
@@ -1982,17 +2007,19 @@ __device__ __attribute__((noinline)) void fill_block_got2(kargs_c* ka, int blk, 
                                    x4 = gload(sp + 256), x5 = gload(sp + 320);
           bool ok = ((unsigned)(x0 >> 32) == ep) && ((unsigned)(x1 >> 32) == ep) && ((unsigned)(x2 >> 32) == ep) &&
                     ((unsigned)(x3 >> 32) == ep) && ((unsigned)(x4 >> 32) == ep) && ((unsigned)(x5 >> 32) == ep);
+          // R~ and D~ carried + 4h, as in pass 1 (the tag bits are unchanged): 2 subtractions per
+          // row-step instead of 3
           Hs1 = (int)(unsigned)x0;
-          Rs1 = (int)(unsigned)x1;
+          Rs1 = (int)(unsigned)x1 + h4;
           U = (int)(unsigned)x2;
           Hs2 = (int)(unsigned)x3;
-          Rs2 = (int)(unsigned)x4;
-          Ds2 = (int)(unsigned)x5;
+          Rs2 = (int)(unsigned)x4 + h4;
+          Ds2 = (int)(unsigned)x5 + h4;
           for (int v = lane; v < nv; v += 64) {
             const unsigned long long gz = gload(brz + 16 * q0 + v), gf = gload(brf + 16 * q0 + v);
             ok = ok && ((unsigned)(gz >> 32) == ep) && ((unsigned)(gf >> 32) == ep);
             *L(lds + v) = (int)(unsigned)gz;
-            *L(lds + 256 + v) = (int)(unsigned)gf;
+            *L(lds + 256 + v) = (int)(unsigned)gf + h4;
           }
           ready = __ballot(!ok) == 0;
           if (!ready) __builtin_amdgcn_s_sleep(8);
@@ -2002,11 +2029,11 @@ __device__ __attribute__((noinline)) void fill_block_got2(kargs_c* ka, int blk, 
         if (lane == 0) atomicExch(a.err, 15);
         q1 = q0;
       }
-      // row 0 (stripe 0), tagged and shifted: H~ 3 at column 0, 2 - 4h right of it; D~ 3 - 4h, 2 - 8h
+      // row 0 (stripe 0), tagged and shifted: H~ 3 at column 0, 2 - 4h right of it; D~ + 4h 3, 2 - 4h
       p2_stage<2>(lds, s, nv, 16 * (q1 - q0), lane,
                   [&](int v, int k) {
                     const int col = cs + 16 * q0 + v;
-                    return col < 0 ? MSA_NEG : (k == 0 ? (col == 0 ? 3 : 2 - h4) : (col == 0 ? 3 - h4 : 2 - 2 * h4));
+                    return col < 0 ? MSA_NEG : (k == 0 ? (col == 0 ? 3 : 2 - h4) : (col == 0 ? 3 : 2 - h4));
                   },
                   a.cod + a.cod_off, a.cod_copy, cs, q0);
       const int tmin = 1 - cs + lane;
@@ -2032,48 +2059,59 @@ __device__ __attribute__((noinline)) void fill_block_got2(kargs_c* ka, int blk, 
         const fl_v4u c4 = p2_codes(lds, q - q0, lane);
         const unsigned cw[4] = {c4.x, c4.y, c4.z, c4.w};
         unsigned dw1[4], dw2[4];
+        // a cell's direction byte, tags of its inputs H~ diag | R~ left << 2 | D~ up << 4: built with
+        // bits 6+ left over (bfi + lshl_or), four bytes gathered by v_perm and masked once per word
+        auto dbyte = [](int Ht, int Rt, int Dt) __attribute__((always_inline)) {
+          unsigned x, y;
+          asm("v_bfi_b32 %0, 3, %1, %2" : "=v"(x) : "v"(Rt), "v"((unsigned)Dt << 2));
+          asm("v_bfi_b32 %0, 3, %1, %2" : "=v"(y) : "v"(Ht), "v"(x << 2));
+          return y;
+        };
+        auto dword = [](unsigned b0, unsigned b1, unsigned b2, unsigned b3) __attribute__((always_inline)) {
+          const unsigned lo = __builtin_amdgcn_perm(b1, b0, 0x0c0c0400u);
+          const unsigned hi = __builtin_amdgcn_perm(b3, b2, 0x0c0c0400u);
+          return __builtin_amdgcn_perm(hi, lo, 0x05040100u) & 0x3f3f3f3fu;
+        };
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const unsigned s4 = __builtin_amdgcn_perm(phi, plo, cw[u]);
           const unsigned s4b = __builtin_amdgcn_perm(phi2, plo2, cw[u]);
-          unsigned word1 = 0, word2 = 0;
+          unsigned by1[4], by2[4];
 #pragma unroll
           for (int kk = 0; kk < 4; ++kk) {
             const int kx = 4 * u + kk;
             const int sc = ((int)(s4 << (24 - 8 * kk))) >> 24;
             const int sb = ((int)(s4b << (24 - 8 * kk))) >> 24;
-            // row 1
+            // row 1 (R~ / D~ carried + 4h: Rs1, uD, and the results rr, dd)
             const int uH = dpp_shr1(INZ[kx], Hs2);
             const int uD = dpp_shr1(INF[kx], Ds2);
             const int t1 = (int)((unsigned)U | 3u) + sc;
-            const int t2 = (int)(((unsigned)Rs1 & ~3u) | 2u);
-            const int t3 = (int)(((unsigned)uD & ~3u) | 1u);
-            word1 |= (((unsigned)U & 3u) | (((unsigned)Rs1 & 3u) << 2) | (((unsigned)uD & 3u) << 4)) << (8 * kk);
-            const int t1h = t1 - h4;
-            int hh1 = imax3(t1, t2, t3);
-            int rr1 = imax3(t1h, t2, t3 - h4);
-            int dd1 = imax3(t1h, t2 - h4, t3);
-            asm("" : "+v"(hh1));
+            const int t2p = (int)(((unsigned)Rs1 & ~3u) | 2u);
+            const int t3p = (int)(((unsigned)uD & ~3u) | 1u);
+            by1[kk] = dbyte(U, Rs1, uD);
+            const int t2 = t2p - h4, t3 = t3p - h4;
+            int hh1 = vmax3(t1, t2, t3);
+            int rr1 = vmax3(t1, t2p, t3);
+            int dd1 = vmax3(t1, t2, t3p);
             // row 2: diagonal = row 1's previous H~, above = row 1's new cell
             const bool before = HEAD && (16 * q + kx < tmin);
             if constexpr (HEAD) {
               hh1 = before ? 1 - h4 : hh1;
-              rr1 = before ? 1 - 2 * h4 : rr1;
-              dd1 = before ? 1 - h4 : dd1;
+              rr1 = before ? 1 - h4 : rr1;
+              dd1 = before ? 1 : dd1;
             }
             const int s1 = (int)((unsigned)Hs1 | 3u) + sb;
-            const int s2 = (int)(((unsigned)Rs2 & ~3u) | 2u);
-            const int s3 = (int)(((unsigned)dd1 & ~3u) | 1u);
-            word2 |= (((unsigned)Hs1 & 3u) | (((unsigned)Rs2 & 3u) << 2) | (((unsigned)dd1 & 3u) << 4)) << (8 * kk);
-            const int s1h = s1 - h4;
-            int hh2 = imax3(s1, s2, s3);
-            int rr2 = imax3(s1h, s2, s3 - h4);
-            int dd2 = imax3(s1h, s2 - h4, s3);
-            asm("" : "+v"(hh2));
+            const int s2p = (int)(((unsigned)Rs2 & ~3u) | 2u);
+            const int s3p = (int)(((unsigned)dd1 & ~3u) | 1u);
+            by2[kk] = dbyte(Hs1, Rs2, dd1);
+            const int s2 = s2p - h4, s3 = s3p - h4;
+            int hh2 = vmax3(s1, s2, s3);
+            int rr2 = vmax3(s1, s2p, s3);
+            int dd2 = vmax3(s1, s2, s3p);
             if constexpr (HEAD) {
               hh2 = before ? 1 - h4 : hh2;
-              rr2 = before ? 1 - 2 * h4 : rr2;
-              dd2 = before ? 1 - h4 : dd2;
+              rr2 = before ? 1 - h4 : rr2;
+              dd2 = before ? 1 : dd2;
             }
             if constexpr (CAP) {
               if (16 * q + kx == tf) {
@@ -2093,8 +2131,8 @@ __device__ __attribute__((noinline)) void fill_block_got2(kargs_c* ka, int blk, 
             Rs2 = rr2;
             Ds2 = dd2;
           }
-          dw1[u] = word1;
-          dw2[u] = word2;
+          dw1[u] = dword(by1[0], by1[1], by1[2], by1[3]);
+          dw2[u] = dword(by2[0], by2[1], by2[2], by2[3]);
         }
         __builtin_nontemporal_store(fl_v4u{dw1[0], dw1[1], dw1[2], dw1[3]}, dp + (size_t)q * 128);
         __builtin_nontemporal_store(fl_v4u{dw2[0], dw2[1], dw2[2], dw2[3]}, dp + (size_t)q * 128 + 64);

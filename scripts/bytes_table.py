@@ -26,7 +26,9 @@ def flow_bytes(d: Path):
         for r in csv.DictReader(open(trace)):
             if "flow_kernel" in r["Kernel_Name"] or "flow_fill" in r["Kernel_Name"]:
                 dur.setdefault(r["Kernel_Name"], []).append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
-    for sub, name, scale in (("pmc_fetch", "FETCH_SIZE", 2.0), ("pmc_write", "WRITE_SIZE", 1.0)):
+    for sub, name, scale in (("pmc_fetch", "FETCH_SIZE", 2.0), ("pmc_write", "WRITE_SIZE", 1.0),
+                             ("pmc_sq", "SQ_INSTS_VALU", 1.0 / 1024.0), ("pmc_sq", "SQ_INSTS_SALU", 1.0 / 1024.0),
+                             ("pmc_sq", "SQ_INSTS_LDS", 1.0 / 1024.0), ("pmc_sq", "SQ_WAVES", 1.0 / 1024.0)):
         f = d / sub / "run_counter_collection.csv"
         if not f.exists():
             continue
@@ -72,7 +74,11 @@ for wl in wls:
         writes_counted=w, fetches_counted=f,
         write_attributed=dict(pass2=w["prod"] - w["abl1"], snap=w["prod"] - w["abl2"], br=w["prod"] - w["abl4"]),
         fetch_attributed=dict(pass2=f["prod"] - f["abl1"], snap=f["prod"] - f["abl2"], br=f["prod"] - f["abl4"]),
-        dur_us={v: runs[v].get("dur_us") for v in runs})
+        dur_us={v: runs[v].get("dur_us") for v in runs},
+        # wave instructions per launch; x 64 lanes / cells = lane-ops per cell (pass 2 = prod - abl1)
+        valu_lane_ops_per_cell={v: 64.0 * tot(v, "SQ_INSTS_VALU") / sz["cells"] for v in runs},
+        salu_wave_instrs_per_64_cells={v: 64.0 * tot(v, "SQ_INSTS_SALU") / sz["cells"] for v in runs},
+        lds_wave_instrs_per_64_cells={v: 64.0 * tot(v, "SQ_INSTS_LDS") / sz["cells"] for v in runs})
 (ROOT / "profiles").mkdir(exist_ok=True)
 for wl, r in res.items():
     (ROOT / "profiles" / f"{rnd}_{wl}_bytes.json").write_text(json.dumps(r, indent=1))

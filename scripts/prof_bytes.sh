@@ -11,3 +11,5 @@ mkdir -p $OUT
 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 scripts/prof_run.py $WL 3
 timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python3 scripts/prof_run.py $WL 2
 timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python3 scripts/prof_run.py $WL 2
+# instruction mix of the same variant (SQ counters share a pass; attributes VALU per pass with MSA_ABL=1)
+timeout -k 10 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY -d $OUT/pmc_sq -o run --output-format csv -- python3 scripts/prof_run.py $WL 2
