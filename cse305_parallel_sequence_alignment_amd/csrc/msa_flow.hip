@@ -69,11 +69,24 @@ namespace msa {
 #ifndef FL_FSLEEP
 #define FL_FSLEEP 32    // s_sleep between a pass-2 wave's polls of its block's last granule
 #endif
+// Affine / Gotoh pass-2 waves claim their blocks in readiness order but long before pass 1 reaches
+// them (pass 1 is the chain): after FL_FSLONG polls a wave polls every FL_FSLEEP2 x 64 cycles instead
+// (ref 10k: ~4 of the kernel's ~32 VALU lane-ops per cell were such polls)
+#ifndef FL_FSLEEP2
+#define FL_FSLEEP2 96
+#endif
+#ifndef FL_FSLONG
+#define FL_FSLONG 8
+#endif
+__device__ __forceinline__ void fl_poll_sleep(int polls) {
+  if (polls < FL_FSLONG) __builtin_amdgcn_s_sleep(FL_FSLEEP);
+  else __builtin_amdgcn_s_sleep(FL_FSLEEP2);
+}
 #ifndef FL_IOSLEEP
 #define FL_IOSLEEP 1    // s_sleep of an idle io wave
 #endif
 // Diagnostic builds only (-DMSA_ABL=mask; results are wrong): 1 no pass-2 work, 2 no SNAP
-// stores, 4 io-out stores no bottom rows (granules still), 16 SW-linear compute waves never wait on their producer
+// stores, 4 io-out stores no bottom rows (granules still), 8 R = 2 pass-2 blocks store no cells, 16 SW-linear compute waves never wait on their producer
 // or consumers (each stripe runs at its own speed), 32 never on the producer, 64 never on consumers
 #ifndef MSA_ABL
 #define MSA_ABL 0
@@ -682,6 +695,8 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
         }
         if (!left) break;
         if (!any) {
+          // (a longer sleep after empty rounds -- s_sleep 4 after two -- cut the polls' VALU but cost C2
+          // 2.7%: 0.4691 vs 0.4565 ms; the last link's granules and BR wait on this wave)
           __builtin_amdgcn_s_sleep(FL_IOSLEEP);
           if (++spins > FL_SPIN_MAX) break;
         }
@@ -1558,7 +1573,7 @@ __device__ __attribute__((noinline)) void fill_block_aff(kargs_c* ka, int blk, i
       for (int t2 = 0; !ready && t2 < (int)(FL_SPIN_MAX >> 2); ++t2) {  // the block's last granules first
         const unsigned long long gz = gload(brz + 16 * q0 + nv - 1), gf = gload(brf + 16 * q0 + nv - 1);
         ready = __ballot((unsigned)(gz >> 32) != ep || (unsigned)(gf >> 32) != ep) == 0;
-        if (!ready) __builtin_amdgcn_s_sleep(FL_FSLEEP);
+        if (!ready) fl_poll_sleep(t2);
       }
       if (ready) {
         ready = false;
@@ -1686,7 +1701,7 @@ __device__ __attribute__((noinline)) void fill_block_aff2(kargs_c* ka, int blk, 
       for (int t2 = 0; !ready && t2 < (int)(FL_SPIN_MAX >> 2); ++t2) {
         const unsigned long long gz = gload(brz + 16 * q0 + nv - 1), gf = gload(brf + 16 * q0 + nv - 1);
         ready = __ballot((unsigned)(gz >> 32) != ep || (unsigned)(gf >> 32) != ep) == 0;
-        if (!ready) __builtin_amdgcn_s_sleep(FL_FSLEEP);
+        if (!ready) fl_poll_sleep(t2);
       }
       if (ready) {
         ready = false;
@@ -1780,8 +1795,10 @@ __device__ __attribute__((noinline)) void fill_block_aff2(kargs_c* ka, int blk, 
           dw1[u] = word1;
           dw2[u] = word2;
         }
-        __builtin_nontemporal_store(fl_v4u{dw1[0], dw1[1], dw1[2], dw1[3]}, dp + (size_t)q * 128);
-        __builtin_nontemporal_store(fl_v4u{dw2[0], dw2[1], dw2[2], dw2[3]}, dp + (size_t)q * 128 + 64);
+        if constexpr ((MSA_ABL & 8) == 0) {
+          __builtin_nontemporal_store(fl_v4u{dw1[0], dw1[1], dw1[2], dw1[3]}, dp + (size_t)q * 128);
+          __builtin_nontemporal_store(fl_v4u{dw2[0], dw2[1], dw2[2], dw2[3]}, dp + (size_t)q * 128 + 64);
+        }
       }
       bb = (row_i <= m) ? best : INT32_MIN;
       bi = row_i;
@@ -1838,7 +1855,7 @@ __device__ __attribute__((noinline)) void fill_block_got(kargs_c* ka, int blk, i
       for (int t2 = 0; !ready && t2 < (int)(FL_SPIN_MAX >> 2); ++t2) {
         const unsigned long long gz = gload(brz + 16 * q0 + nv - 1), gf = gload(brf + 16 * q0 + nv - 1);
         ready = __ballot((unsigned)(gz >> 32) != ep || (unsigned)(gf >> 32) != ep) == 0;
-        if (!ready) __builtin_amdgcn_s_sleep(FL_FSLEEP);
+        if (!ready) fl_poll_sleep(t2);
       }
 #ifdef MSA_STAMPS
       tp1 = __builtin_amdgcn_s_memtime();
@@ -1998,7 +2015,7 @@ __device__ __attribute__((noinline)) void fill_block_got2(kargs_c* ka, int blk, 
       for (int t2 = 0; !ready && t2 < (int)(FL_SPIN_MAX >> 2); ++t2) {
         const unsigned long long gz = gload(brz + 16 * q0 + nv - 1), gf = gload(brf + 16 * q0 + nv - 1);
         ready = __ballot((unsigned)(gz >> 32) != ep || (unsigned)(gf >> 32) != ep) == 0;
-        if (!ready) __builtin_amdgcn_s_sleep(FL_FSLEEP);
+        if (!ready) fl_poll_sleep(t2);
       }
       if (ready) {
         ready = false;
@@ -2134,8 +2151,10 @@ __device__ __attribute__((noinline)) void fill_block_got2(kargs_c* ka, int blk, 
           dw1[u] = dword(by1[0], by1[1], by1[2], by1[3]);
           dw2[u] = dword(by2[0], by2[1], by2[2], by2[3]);
         }
-        __builtin_nontemporal_store(fl_v4u{dw1[0], dw1[1], dw1[2], dw1[3]}, dp + (size_t)q * 128);
-        __builtin_nontemporal_store(fl_v4u{dw2[0], dw2[1], dw2[2], dw2[3]}, dp + (size_t)q * 128 + 64);
+        if constexpr ((MSA_ABL & 8) == 0) {
+          __builtin_nontemporal_store(fl_v4u{dw1[0], dw1[1], dw1[2], dw1[3]}, dp + (size_t)q * 128);
+          __builtin_nontemporal_store(fl_v4u{dw2[0], dw2[1], dw2[2], dw2[3]}, dp + (size_t)q * 128 + 64);
+        }
       };
       using T_ = std::true_type;
       using F_ = std::false_type;

@@ -33,6 +33,27 @@ __global__ void st_nt16x2(v4u* out) {
     v.x += 1;
   }
 }
+// the R = 2 pattern paced like pass 2 (one 2 KiB phase per ~1,000 cycles), 16 KiB blocks claimed from a
+// counter in stripe-interleaved order over a buffer larger than the Infinity Cache
+__global__ void st_paced(v4u* out, int* ticket, int nblk, int nseg) {
+  const int lane = threadIdx.x & 63;
+  for (;;) {
+    int t = 0;
+    if (lane == 0) t = atomicAdd(ticket, 1);
+    t = __builtin_amdgcn_readlane(t, 0);
+    if (t >= nblk) break;
+    const int s = t % (nblk / nseg), seg = t / (nblk / nseg);  // block (stripe s, segment seg)
+    v4u* p = out + ((size_t)s * nseg + seg) * 1024 + lane;    // 16 KiB per block
+    v4u v = {(unsigned)lane, (unsigned)t, 2u, 3u};
+    for (int q = 0; q < 8; ++q) {
+      __builtin_amdgcn_s_sleep(15);
+      __builtin_nontemporal_store(v, p + (size_t)q * 128);
+      v.y += 1;
+      __builtin_nontemporal_store(v, p + (size_t)q * 128 + 64);
+      v.x += 1;
+    }
+  }
+}
 __global__ void st_g8(unsigned long long* out) {
   const int lane = threadIdx.x & 63;
   const size_t wave = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
@@ -74,6 +95,13 @@ int main() {
                        (unsigned long long*)sink);
     (void)hipMemsetAsync(b, 2, 512ull << 20, 0);
     hipLaunchKernelGGL(ld_16, dim3(waves / wpb), dim3(64 * wpb), 0, 0, (const v4u*)a, (unsigned*)sink);
+  }
+  // 400 MiB (C5's plane) as 25,600 blocks of 16 KiB, 160 stripes x 160 segments
+  int* tk;
+  if (hipMalloc(&tk, 8) != hipSuccess) return 1;
+  for (int r = 0; r < 2; ++r) {
+    (void)hipMemsetAsync(tk, 0, 8, 0);
+    hipLaunchKernelGGL(st_paced, dim3(1024), dim3(256), 0, 0, (v4u*)b, tk, 25600, 160);
   }
   if (hipDeviceSynchronize() != hipSuccess) { printf("failed\n"); return 1; }
   printf("ok: each kernel moves %zu bytes\n", kBytes);

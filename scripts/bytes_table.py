@@ -4,14 +4,14 @@ scripts/prof_bytes.sh runs on the production library and on MSA_ABL ablation bui
 1 = no pass-2 work, 2 = no SNAP stores, 4 = no bottom-row (BR) stores), against the buffer sizes the
 plan allocates.  Prints one JSON object (and writes profiles/<round>_<wl>_bytes.json):
 
-    python scripts/bytes_table.py gpurun_out r05 ref c5
+    python scripts/bytes_table.py gpurun_out/pb2 r05 ref c5     (runs gpurun_out/pb2_<wl>_<variant>)
 """
 import csv
 import json
 import sys
 from pathlib import Path
 
-src, rnd = Path(sys.argv[1]), sys.argv[2]
+prefix, rnd = sys.argv[1], sys.argv[2]
 wls = sys.argv[3:] or ["ref", "c5"]
 ROOT = Path(__file__).resolve().parent.parent
 
@@ -61,7 +61,8 @@ def sizes(wl: str):
 
 res = {}
 for wl in wls:
-    runs = {v: flow_bytes(src / f"pb_{wl}_{v}") for v in ("prod", "abl1", "abl2", "abl4")}
+    runs = {v: flow_bytes(Path(f"{prefix}_{wl}_{v}")) for v in ("prod", "abl1", "abl2", "abl4", "abl8")
+            if Path(f"{prefix}_{wl}_{v}", "pmc_write").exists()}
     sz = sizes(wl)
 
     def tot(v, key):
@@ -72,8 +73,14 @@ for wl in wls:
     res[wl] = dict(
         buffers_bytes=sz,
         writes_counted=w, fetches_counted=f,
-        write_attributed=dict(pass2=w["prod"] - w["abl1"], snap=w["prod"] - w["abl2"], br=w["prod"] - w["abl4"]),
-        fetch_attributed=dict(pass2=f["prod"] - f["abl1"], snap=f["prod"] - f["abl2"], br=f["prod"] - f["abl4"]),
+        # prod - abl1 = pass 2's bytes; prod - abl8 = pass 2's cell stores alone; abl1 = pass 1's (BR, SNAP, granules)
+        write_attributed={k: w["prod"] - w[v] for k, v in (("pass2", "abl1"), ("snap", "abl2"), ("br", "abl4"),
+                                                           ("pass2_cells", "abl8")) if v in w},
+        fetch_attributed={k: f["prod"] - f[v] for k, v in (("pass2", "abl1"), ("snap", "abl2"), ("br", "abl4"),
+                                                           ("pass2_cells", "abl8")) if v in f},
+        pass1_writes_vs_buffers=(w["abl1"] / (sz["br"] + sz["snap"] + sz["granules"])) if "abl1" in w else None,
+        pass2_writes_vs_plane=((w["prod"] - w["abl1"]) / sz["plane"]) if "abl1" in w else None,
+        traffic_vs_plane=(w["prod"] + f["prod"]) / sz["plane"],
         dur_us={v: runs[v].get("dur_us") for v in runs},
         # wave instructions per launch; x 64 lanes / cells = lane-ops per cell (pass 2 = prod - abl1)
         valu_lane_ops_per_cell={v: 64.0 * tot(v, "SQ_INSTS_VALU") / sz["cells"] for v in runs},

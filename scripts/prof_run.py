@@ -20,11 +20,13 @@ if wl in ("c2", "c2n"):
     A, B = seqs[1][:10000], seqs[0][:10000]
     cells = LB.CELLS_H if wl == "c2" else LB.CELLS_NONE
     pl = Plan(LB.SW_LINEAR, cells, [10000], [10000], [0], [0], match=1, mismatch=0, gap_open=1, gap_extend=1)
-elif wl == "c5":
+elif wl in ("c5", "c5h"):
     from cse305_parallel_sequence_alignment_amd import data
 
-    A, B = data.c5_pair(0, False)  # the bench's C5 pair
-    pl = Plan(LB.SW_AFFINE, LB.CELLS_DIR, [20000], [20000], [0], [0], match=1, mismatch=0, gap_open=3,
+    A, B = data.c5_pair(0, False)  # the bench's C5 pair (c5h: its first 10k x 10k, a plane under the L3's size)
+    if wl == "c5h":
+        A, B = A[:10000], B[:10000]
+    pl = Plan(LB.SW_AFFINE, LB.CELLS_DIR, [len(A)], [len(B)], [0], [0], match=1, mismatch=0, gap_open=3,
               gap_extend=1, track_end=True)
 elif wl in ("ref", "ref20", "refwhole"):
     L = {"ref": 10000, "ref20": 20000, "refwhole": None}[wl]
@@ -51,13 +53,13 @@ if pl.cells != LB.CELLS_NONE:
     out = torch.empty(pl.cells_elems, dtype=torch.uint8 if pl.cells == LB.CELLS_DIR else torch.int32, device="cuda")
 dA, dB = enc(A), enc(B)
 tb = None
-if wl in ("c5", "ref", "ref20", "refwhole"):  # the bench's step: fill, then the traceback walk on the device
+if wl in ("c5", "c5h", "ref", "ref20", "refwhole"):  # the bench's step: fill, then the traceback walk on the device
     tb = (torch.empty(len(A) + len(B) + 2, dtype=torch.uint8, device="cuda"),
           torch.zeros(8, dtype=torch.int64, device="cuda"))
 for _ in range(reps):
     pl.run(dA, dB, out)
     if tb is not None:
-        if wl == "c5":
+        if wl in ("c5", "c5h"):
             pl.traceback_async(out, *tb)
         else:
             pl.traceback_gotoh_async(out, *tb, -1)

@@ -84,6 +84,9 @@ for cpl in range(min(4, ncpl)):
         nslow_mean=round(float(np.mean([r["nslow"] for r in rows])), 1),
         wait_in_share=round(float(np.mean([r["tw_in"] / 2400.0 / max(1e-9, d) for r, d in zip(rows, durs)])), 3),
         wait_cons_share=round(float(np.mean([r["tw_cons"] / 2400.0 / max(1e-9, d) for r, d in zip(rows, durs)])), 3),
-        claim_minus_start_us=[round(c - s, 1) for c, s in zip(claims, starts[ks % W == 0])][:16]))
+        claim_minus_start_us=[round(c - s, 1) for c, s in zip(claims, starts[ks % W == 0])][:16],
+        # per item boundary (item g-1 -> g): the start lag of its first stripe, in phases
+        cross_lags_phases=[round(float(lag[i]) / ph, 1) for i in range(len(lag)) if ks[i + 1] % W == 0],
+        item_starts_us=[round(float(t), 1) for t, k in zip(starts, ks) if k % W == 0]))
 res["chains"] = chains
 print(json.dumps(res))
