@@ -374,13 +374,17 @@ __device__ __forceinline__ FillArgs fill_args_of(kargs_c* k) {
 #endif
   };
 }
-template <bool FLOOR, bool TRACKPOS, int R>
+// Pass-2 block functions, one instantiation per calling kernel (CALLER 0: flow_kernel's in-launch pass 2,
+// 1: flow_fill_kernel): a non-inlined function shared by two kernels gets the tighter register budget of
+// the two (flow_fill_kernel's four waves per SIMD = 128 VGPRs), and spilled there -- fill_block_aff2 188 B
+// and fill_block_got2 68 B of scratch per lane, which was C5's and ref's unexplained HBM traffic
+template <bool FLOOR, bool TRACKPOS, int R, int CALLER>
 // SW-linear pass-2 blocks take their arguments by value (C2 0.4646 -> 0.4604 ms against the kernarg pointer)
 __device__ __attribute__((noinline)) void fill_block(const FillArgs fa, int blk, int lane, lds_int* lds);
-__device__ __attribute__((noinline)) void fill_block_aff(kargs_c* ka, int blk, int lane, lds_int* lds);
-__device__ __attribute__((noinline)) void fill_block_aff2(kargs_c* ka, int blk, int lane, lds_int* lds);
-__device__ __attribute__((noinline)) void fill_block_got(kargs_c* ka, int blk, int lane, lds_int* lds);
-__device__ __attribute__((noinline)) void fill_block_got2(kargs_c* ka, int blk, int lane, lds_int* lds);
+template <int CALLER> __device__ __attribute__((noinline)) void fill_block_aff(kargs_c* ka, int blk, int lane, lds_int* lds);
+template <int CALLER> __device__ __attribute__((noinline)) void fill_block_aff2(kargs_c* ka, int blk, int lane, lds_int* lds);
+template <int CALLER> __device__ __attribute__((noinline)) void fill_block_got(kargs_c* ka, int blk, int lane, lds_int* lds);
+template <int CALLER> __device__ __attribute__((noinline)) void fill_block_got2(kargs_c* ka, int blk, int lane, lds_int* lds);
 
 template <bool FLOOR, bool BEST, bool SAVE, bool TRACKPOS, int R = 1, int FK = 0>
 #ifndef FL_WPE
@@ -459,11 +463,11 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
         if (t >= a.nblk) break;
         kargs_c* ka = (kargs_c*)__builtin_amdgcn_kernarg_segment_ptr();  // (a is the only argument)
         lds_int* wl = L(smem + w * FL_P2INTS);
-        if constexpr (GOT && R == 2) fill_block_got2(ka, a.border[t], lane, wl);
-        else if constexpr (GOT) fill_block_got(ka, a.border[t], lane, wl);
-        else if constexpr (AFF && R == 2) fill_block_aff2(ka, a.border[t], lane, wl);
-        else if constexpr (AFF) fill_block_aff(ka, a.border[t], lane, wl);
-        else fill_block<FLOOR, TRACKPOS, R>(fill_args_of(ka), a.border[t], lane, wl);
+        if constexpr (GOT && R == 2) fill_block_got2<0>(ka, a.border[t], lane, wl);
+        else if constexpr (GOT) fill_block_got<0>(ka, a.border[t], lane, wl);
+        else if constexpr (AFF && R == 2) fill_block_aff2<0>(ka, a.border[t], lane, wl);
+        else if constexpr (AFF) fill_block_aff<0>(ka, a.border[t], lane, wl);
+        else fill_block<FLOOR, TRACKPOS, R, 0>(fill_args_of(ka), a.border[t], lane, wl);
       }
 #ifdef MSA_STAMPS
       wg_stamp(1, __builtin_amdgcn_s_memrealtime());
@@ -1389,7 +1393,7 @@ __device__ __forceinline__ fl_v4u p2_codes(lds_int* lds, int k, int lane) {
 // for the block's last bottom-row granule, then loads and checks them all.
 // R = 2: lane r holds rows 128s+2r+1 (X/U) and 128s+2r+2 (X2); cells go to the
 // R = 2 layout (per 4 steps: the wave's row-1 int4s, then its row-2 int4s).
-template <bool FLOOR, bool TRACKPOS, int R>
+template <bool FLOOR, bool TRACKPOS, int R, int CALLER>
 __device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, int lane, lds_int* lds) {
   constexpr bool GS = !FLOOR;
   const unsigned ep = a.ep;
@@ -1546,6 +1550,7 @@ __device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, 
 // phase are one 16-byte store, a wave's phase one contiguous 1 KiB -- and reduces its first
 // maximum H = H~ - e(i+j).  The bytes are stripe_kernel's MSA_ALG_SWA bytes (the walk
 // traceback_kernel<TB_SW> reads them unchanged).
+template <int CALLER>
 __device__ __attribute__((noinline)) void fill_block_aff(kargs_c* ka, int blk, int lane, lds_int* lds) {
   const FillArgs a = fill_args_of(ka);
   const unsigned ep = a.ep;
@@ -1672,6 +1677,7 @@ __device__ __attribute__((noinline)) void fill_block_aff(kargs_c* ka, int blk, i
 // above (Z, F~) from the previous lane's row 2 (lane 0: the stripe above's bottom row), row 2 from
 // row 1 at the same column and its diagonal from row 1's previous Z.  A phase's bytes go out as
 // one 2 KiB block (row-1 segments, then row-2 segments: traceback_kernel<TB_SW, 2>'s layout).
+template <int CALLER>
 __device__ __attribute__((noinline)) void fill_block_aff2(kargs_c* ka, int blk, int lane, lds_int* lds) {
   const FillArgs a = fill_args_of(ka);
   const unsigned ep = a.ep;
@@ -1825,6 +1831,7 @@ __device__ __attribute__((noinline)) void fill_block_aff2(kargs_c* ka, int blk, 
 // layout.  The block holding cell (m, n) stores its three tables, unshifted, as the last
 // stripe's final state (reduce_pairs_kernel turns it into the pair result, the walk reads
 // find_alignment's end rule from it).
+template <int CALLER>
 __device__ __attribute__((noinline)) void fill_block_got(kargs_c* ka, int blk, int lane, lds_int* lds) {
   const FillArgs a = fill_args_of(ka);
   const unsigned ep = a.ep;
@@ -1987,6 +1994,7 @@ __device__ __attribute__((noinline)) void fill_block_got(kargs_c* ka, int blk, i
 // from the previous lane's row 2 (lane 0: the stripe above's bottom row), row 2 from row 1 at the same
 // column, its diagonal from row 1's previous cell.  A phase's bytes go out as one 2 KiB block: the
 // wave's row-1 16-byte segments, then its row-2 segments (traceback_kernel's R = 2 layout).
+template <int CALLER>
 __device__ __attribute__((noinline)) void fill_block_got2(kargs_c* ka, int blk, int lane, lds_int* lds) {
   const FillArgs a = fill_args_of(ka);
   const unsigned ep = a.ep;
@@ -2190,11 +2198,11 @@ __global__ __launch_bounds__(FL_FILLW * 64) __attribute__((amdgpu_waves_per_eu(F
     if (lane == 0) t = atomicAdd(a.ticket + MSA_TK_BLOCK, 1);
     t = __builtin_amdgcn_readlane(t, 0);
     if (t >= a.nblk) break;
-    if constexpr (FK == 2 && R == 2) fill_block_got2(ka, a.border[t], lane, wl);
-    else if constexpr (FK == 2) fill_block_got(ka, a.border[t], lane, wl);
-    else if constexpr (FK == 1 && R == 2) fill_block_aff2(ka, a.border[t], lane, wl);
-    else if constexpr (FK == 1) fill_block_aff(ka, a.border[t], lane, wl);
-    else fill_block<FLOOR, TRACKPOS, R>(fill_args_of(ka), a.border[t], lane, wl);
+    if constexpr (FK == 2 && R == 2) fill_block_got2<1>(ka, a.border[t], lane, wl);
+    else if constexpr (FK == 2) fill_block_got<1>(ka, a.border[t], lane, wl);
+    else if constexpr (FK == 1 && R == 2) fill_block_aff2<1>(ka, a.border[t], lane, wl);
+    else if constexpr (FK == 1) fill_block_aff<1>(ka, a.border[t], lane, wl);
+    else fill_block<FLOOR, TRACKPOS, R, 1>(fill_args_of(ka), a.border[t], lane, wl);
   }
 }
 
