@@ -18,7 +18,7 @@ from pathlib import Path
 src, wl, rnd = Path(sys.argv[1]), sys.argv[2], sys.argv[3]
 # the DP kernel of the workload: flow_kernel (single-pair SW linear, pass 1 + pass-2
 # blocks in one launch) or stripe_kernel (everything else)
-KERNELS = ("flow_kernel", "stripe_kernel", "band_kernel")
+KERNELS = ("flow_kernel", "stripe_kernel", "band_kernel", "cflow_kernel")
 dst = Path(__file__).resolve().parent.parent / "profiles"
 dst.mkdir(exist_ok=True)
 
@@ -50,20 +50,22 @@ def _keep(durs):
     return {d for d, t in durs.items() if t >= KEEP_FRAC * top}
 
 
-def per_dispatch(sub):
+def per_dispatch(sub, match=None):
     f = src / sub / "run_counter_collection.csv"
     if not f.exists():
         return {}
+    match = match or _is_main
     acc = defaultdict(lambda: defaultdict(float))
     durs = {}
     for r in csv.DictReader(open(f)):
-        if not _is_main(r["Kernel_Name"]):
+        if not match(r["Kernel_Name"]):
             continue
         acc[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
         if "Start_Timestamp" in r and r["Start_Timestamp"]:
             durs[r["Dispatch_Id"]] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
     keep = _keep(durs) if durs else None
-    selection[sub] = dict(dispatches=len(durs) or None, kept=len(keep) if keep is not None else None)
+    if match is _is_main:
+        selection[sub] = dict(dispatches=len(durs) or None, kept=len(keep) if keep is not None else None)
     out = {}
     for k, v in acc.items():
         vals = [x for d, x in v.items() if keep is None or d in keep]
@@ -102,6 +104,15 @@ if "FETCH_SIZE" in pl or "WRITE_SIZE" in pl:
     fetch = 2.0 * pl.get("FETCH_SIZE", 0.0) * 1024.0
     write = pl.get("WRITE_SIZE", 0.0) * 1024.0
     out["hbm_bytes_per_launch"] = {"fetch_corrected": fetch, "write": write, "total": fetch + write}
+    # a long pair's pass 2 is a launch of its own (flow_fill_kernel) inside the same timed DP region:
+    # its bytes belong to the same per-run traffic
+    fill = {}
+    for sub in ("pmc_fetch", "pmc_write"):
+        fill.update(per_dispatch(sub, lambda name: "flow_fill_kernel" in name))
+    if fill:
+        ff, fw = 2.0 * fill.get("FETCH_SIZE", 0.0) * 1024.0, fill.get("WRITE_SIZE", 0.0) * 1024.0
+        h = out["hbm_bytes_per_launch"]
+        h.update(fill_fetch_corrected=ff, fill_write=fw, dp_kernel_only_total=h["total"], total=h["total"] + ff + fw)
 # where the DP kernel's waves spend their time (SQ counters summed over waves; WAIT_ANY +
 # WAIT_INST_ANY + ACTIVE_INST_ANY ~= WAVE_CYCLES, MI355X_MICROARCH.md "rocprofv3 PMC slots"):
 # parked on s_waitcnt / s_barrier, stalled at issue, issuing VALU, issuing LDS
