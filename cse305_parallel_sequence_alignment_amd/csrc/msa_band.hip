@@ -297,6 +297,12 @@ __global__ __launch_bounds__((BK_W + 1) * 64) void band_kernel(KArgs a) {
       const unsigned a_prog_me = lds_addr(prog_me);
       const bool outp = (k >= ks0) && (a.outH != nullptr);
       int32_t* const orow = a.outH + pd.out_off + (size_t)k * pd.pmax * MSA_K * 64 + 4 * lane;
+      // chunked, chunk >= 1, int16 chunk cells (msa_plan_create): H relative to the guessed row, 2 B per
+      // cell, widened by chunk_add_kernel
+      const bool o16 = chunked && c >= 1 && a.outH16 != nullptr;
+      // (MSA_H16_PAIRED: a lane's cells of u-blocks 2h and 2h+1 side by side, one 16-B store per two
+      // u-blocks; chunk_add_kernel undoes the pairing)
+      int16_t* const orow16 = a.outH16 + (size_t)(k - C) * pd.pmax * MSA_K * 64 + (MSA_H16_PAIRED ? 8 : 4) * lane;
       unsigned plo, phi;
       {
         const int sm = 1 + 2 * g + hh, sx = 2 * g + hh;  // f + 2g + h, f = 1 on a match
@@ -406,6 +412,7 @@ __global__ __launch_bounds__((BK_W + 1) * 64) void band_kernel(KArgs a) {
           mask_in(q, Zi, Fi);
         }
         int xz[16], xf[16], ho[16];
+        fl_v2u h16lo = {0u, 0u};
         int pubn = 0;
         const int ctq = ct0 - 16 * g * q;
         const unsigned cw[4] = {Cl.x, Cl.y, Ch.x, Ch.y};
@@ -452,8 +459,23 @@ __global__ __launch_bounds__((BK_W + 1) * 64) void band_kernel(KArgs a) {
           }
 #ifndef BK_NOSTORE
           if (outp) {
-            const msa_v4i hv = {ho[4 * u], ho[4 * u + 1], ho[4 * u + 2], ho[4 * u + 3]};
-            __builtin_nontemporal_store(hv, reinterpret_cast<msa_v4i*>(orow + (size_t)(4 * q + u) * 256));
+            if (o16) {
+              const fl_v2u hv = {__builtin_amdgcn_perm((unsigned)ho[4 * u + 1], (unsigned)ho[4 * u], 0x05040100u),
+                                 __builtin_amdgcn_perm((unsigned)ho[4 * u + 3], (unsigned)ho[4 * u + 2], 0x05040100u)};
+              if constexpr (MSA_H16_PAIRED) {
+                if (u & 1) {
+                  const fl_v4u hp = {h16lo.x, h16lo.y, hv.x, hv.y};
+                  __builtin_nontemporal_store(hp, reinterpret_cast<fl_v4u*>(orow16 + (size_t)(2 * q + (u >> 1)) * 512));
+                } else {
+                  h16lo = hv;
+                }
+              } else {
+                __builtin_nontemporal_store(hv, reinterpret_cast<fl_v2u*>(orow16 + (size_t)(4 * q + u) * 256));
+              }
+            } else {
+              const msa_v4i hv = {ho[4 * u], ho[4 * u + 1], ho[4 * u + 2], ho[4 * u + 3]};
+              __builtin_nontemporal_store(hv, reinterpret_cast<msa_v4i*>(orow + (size_t)(4 * q + u) * 256));
+            }
           }
 #endif
         }

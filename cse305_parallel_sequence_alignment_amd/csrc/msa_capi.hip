@@ -541,6 +541,8 @@ struct msa_plan {
   int* d_dk = nullptr;    // per-chunk constant d_k
   int* d_okk = nullptr;   // per-chunk converged flag
   int* d_skip = nullptr;  // 1: every chunk converged (the exact launch exits)
+  bool h16 = false;       // band_kernel chunks >= 1 write int16 cells to d_h16 (chunk_add_kernel widens)
+  int16_t* d_h16 = nullptr;
 
   void note_stream(hipStream_t s) {
     if (std::find(streams.begin(), streams.end(), s) == streams.end()) streams.push_back(s);
@@ -1049,6 +1051,18 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
         P->grid = std::max(1, std::min(kp.n_items, ncu * bocc));
         P->band_items = std::max(P->band_items, kp.n_items);
         P->ckw = (2 * band + 1 + 3) & ~3;
+        // int16 chunk cells: a chunk >= 1 starts from its guessed row (H <= -h, inside the band >= -h - g band)
+        // at row r0 > band + 64, so an in-band cell (i, j) is reached from (r0, j - i + r0), in the band, along
+        // its diagonal: -h - g band <= H <= i - r0 - h.  Both bounds fit int16 with room when rows + h + g band
+        // stays under 30,000 (C3: 2,112 + 2 + 512); the cells are then written as 2 B, and chunk_add_kernel
+        // reads 2 B and writes 4 B per cell instead of reading and re-writing 4 B.  MSA_BAND_H16=0 (diagnostic)
+        // keeps int32 cells.
+        static const bool h16_on = [] {
+          const char* e = std::getenv("MSA_BAND_H16");
+          return !(e && std::atoi(e) == 0);
+        }();
+        const long long rows = (long long)(warm + cc) * 64 + 64;
+        P->h16 = h16_on && kp.h >= 0 && kp.gap_ext >= 0 && rows + kp.h + (long long)kp.gap_ext * band <= 30000;
       }
     }
   }
@@ -1163,6 +1177,13 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     if (!P->alloc(&P->d_dk, sizeof(int) * P->n_chunks) || !P->alloc(&P->d_okk, sizeof(int) * P->n_chunks) ||
         !P->alloc(&P->d_skip, 64))
       return fail();
+    if (P->h16 && out_mode == MSA_OUT_H) {
+      const msa_pair_desc& pd = P->pairs[0];
+      const int S = (int)((pd.m + 63) / 64);
+      const size_t per = (size_t)pd.pmax * MSA_K * 64;
+      if (S > P->kp.chunk_c && !P->alloc(&P->d_h16, sizeof(int16_t) * per * (size_t)(S - P->kp.chunk_c))) return fail();
+    }
+    if (!P->d_h16) P->h16 = false;
   }
   if (hipEventCreate(&P->ev0) != hipSuccess || hipEventCreate(&P->ev1) != hipSuccess) return fail();
   // the memsets above went to the null stream, which does not order the non-blocking
@@ -1256,6 +1277,7 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
   if (P->chunked) {
     a.ck = P->d_ck;
     a.ckw = P->ckw;
+    if (P->h16 && P->d.cells == MSA_CELLS_H) a.outH16 = P->d_h16;
   }
   hipLaunchKernelGGL(P->fn, dim3(P->grid), dim3(P->threads), P->lds_bytes, st, a);
   HIPCHK(hipGetLastError());
@@ -1268,7 +1290,8 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
                        P->d_okk);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(chunk_add_kernel, dim3(32, P->n_chunks), dim3(256), 0, st,
-                       P->d.cells == MSA_CELLS_H ? a.outH : (int32_t*)nullptr, (const msa_pair_desc*)P->d_pairs,
+                       P->d.cells == MSA_CELLS_H ? a.outH : (int32_t*)nullptr, (const int16_t*)a.outH16,
+                       (const msa_pair_desc*)P->d_pairs,
                        P->d_meta, (const int*)P->d_dk, (const int*)P->d_okk, P->n_chunks, P->kp.chunk_c, P->d_skip,
                        P->d_ticket);
     HIPCHK(hipGetLastError());
@@ -1280,6 +1303,7 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
     if (ep2 == 0) ep2 = g_epoch.fetch_add(1) + 1;
     b.kp.epoch = ep2;
     b.ck = nullptr;
+    b.outH16 = nullptr;  // the exact launch writes every cell as int32
     b.skip = P->d_skip;
     hipLaunchKernelGGL(P->fb_fn, dim3(P->fb_grid), dim3(P->fb_threads), P->fb_lds, st, b);
     HIPCHK(hipGetLastError());
@@ -1342,7 +1366,7 @@ int msa_plan_run_info(msa_plan* P, int32_t* out4, void* stream) {
   out4[0] = P->chunked ? 2 : (P->flow ? 1 : 0);
   out4[1] = P->n_chunks;
   out4[2] = -1;
-  out4[3] = P->chunked ? P->kp.chunk_warm : 0;
+  out4[3] = P->chunked ? (P->kp.chunk_warm | (P->h16 ? (1 << 16) : 0)) : 0;  // bit 16: int16 chunk cells
   if (P->chunked) {
     int v = 0;
     hipStream_t st = (hipStream_t)stream;

@@ -181,7 +181,13 @@ struct KArgs {
   int* ck;                   // [chunk][2: warm-up end, chunk end][2: H, F][ckw] band states
   int ckw;                   // entries per band row (2*band + 1, padded)
   const int* skip;           // exact single-mode launch: exit at once when *skip != 0
+  // chunked banded mode with int16 chunk cells: chunks >= 1 write H relative to their guessed row as
+  // int16 here ([stripe - chunk_c][pmax * 16 * 64], the outH cell order); chunk_add_kernel widens them
+  int16_t* outH16;
 };
+#ifndef MSA_H16_PAIRED
+#define MSA_H16_PAIRED 1  // int16 chunk cells: two u-blocks of a lane per 16 B (msa_band.hip)
+#endif
 
 template <int ALG>
 __device__ __forceinline__ void border_top(const msa_kparams& kp, int c, int (&v)[3], int r0 = 0) {
@@ -1518,9 +1524,11 @@ __global__ __launch_bounds__(256) void chunk_check_kernel(const int* __restrict_
 // [k*chunk_c, (k+1)*chunk_c), contiguous in the layout) and, for the stripe holding row m,
 // to the final state.  If any chunk did not converge nothing is added, *skip = 0 and the
 // tickets are reset: the exact single-mode launch queued next recomputes the pair.
-__global__ __launch_bounds__(256) void chunk_add_kernel(int32_t* H, const msa_pair_desc* pairs, msa_stripe_meta* meta,
-                                                        const int* dk, const int* okk, int n_chunks, int chunk_c,
-                                                        int* skip, int* ticket) {
+// H16 (band_kernel's int16 chunk cells, KArgs::outH16): chunk k >= 1's cells are read from there
+// (2 B per cell) and written widened to H (4 B) -- 6 B per cell instead of the in-place 8 B.
+__global__ __launch_bounds__(256) void chunk_add_kernel(int32_t* H, const int16_t* H16, const msa_pair_desc* pairs,
+                                                        msa_stripe_meta* meta, const int* dk, const int* okk,
+                                                        int n_chunks, int chunk_c, int* skip, int* ticket) {
   const int k = blockIdx.y;
   const msa_pair_desc pd = pairs[0];
   const int S = (pd.m + 63) / 64;
@@ -1558,15 +1566,61 @@ __global__ __launch_bounds__(256) void chunk_add_kernel(int32_t* H, const msa_pa
   }
   __syncthreads();
   const int e = sh_e;
-  if (!sh_ok || e == 0 || H == nullptr) return;
+  const bool wide = (H16 != nullptr && k >= 1);  // this chunk's cells are int16 in H16
+  if (!sh_ok || H == nullptr || (e == 0 && !wide)) return;
   const int ks0 = k * chunk_c, ke = min(S, ks0 + chunk_c);
   const size_t per = (size_t)pd.pmax * MSA_K * 64;  // int32 cells per stripe
   msa_v4i* p = reinterpret_cast<msa_v4i*>(H + pd.out_off + (size_t)ks0 * per);
   const size_t nv = (size_t)(ke - ks0) * per / 4;  // per is a multiple of 1024: nv of 256
+  const size_t step = (size_t)gridDim.x * 1024;
+  if (wide) {
+    // every load and every store instruction covers whole 128-B lines (16-B loads feeding two 16-B stores
+    // 32 B apart wrote every other 16 B of a line per instruction: 190 vs 145 us for C3's in-place int32
+    // add); plain loads, the int16 cells were just written and are partly in the MALL.
+    // MSA_H16_PAIRED: int16 16-B group G = (b, lane) holds the lane's 4 cells of u-blocks 2b and 2b + 1
+    // (int32 16-B groups (2b, lane) and (2b + 1, lane), 64 groups per u-block); else 8-B group x = the
+    // int32 16-B group x.
+    typedef int v2i_t __attribute__((ext_vector_type(2)));
+    auto widen = [&](int lo, int hi) __attribute__((always_inline)) {
+      return msa_v4i{(lo << 16 >> 16) + e, (lo >> 16) + e, (hi << 16 >> 16) + e, (hi >> 16) + e};
+    };
+    if constexpr (MSA_H16_PAIRED) {
+      // one 8-B half of a pair group per thread (8-B loads, as below: 16-B loads feeding two stores 1 KB
+      // apart took 146 vs 134 us): half h of group (b, lane) -> int32 group (2b + h, lane); a wave's
+      // store covers 32 lanes' 16 B of two u-blocks, whole lines
+      const v2i_t* q = reinterpret_cast<const v2i_t*>(H16 + (size_t)(ks0 - chunk_c) * per);
+      for (size_t x0 = (size_t)blockIdx.x * 1024 + threadIdx.x; x0 < nv; x0 += step) {  // 4 loads in flight
+        v2i_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (x0 + 256 * u < nv) v[u] = q[x0 + 256 * u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const size_t x = x0 + 256 * u;
+          if (x < nv) {
+            const size_t G = x >> 1;
+            const size_t o = 2 * G - (G & 63) + 64 * (x & 1);  // (2b + h) * 64 + lane
+            __builtin_nontemporal_store(widen(v[u].x, v[u].y), p + o);
+          }
+        }
+      }
+    } else {
+      const v2i_t* q = reinterpret_cast<const v2i_t*>(H16 + (size_t)(ks0 - chunk_c) * per);
+      for (size_t x0 = (size_t)blockIdx.x * 1024 + threadIdx.x; x0 < nv; x0 += step) {  // 4 loads in flight
+        v2i_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (x0 + 256 * u < nv) v[u] = q[x0 + 256 * u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (x0 + 256 * u < nv) __builtin_nontemporal_store(widen(v[u].x, v[u].y), p + x0 + 256 * u);
+      }
+    }
+    return;
+  }
   // Plain loads: the band the chunk launch just streamed out is partly still in the MALL, so
   // they read ~3% faster than non-temporal ones (C3 0.649 vs 0.674 ms); measured the same or
   // slower: 8 loads in flight, plain stores, the last-written cells first.
-  const size_t step = (size_t)gridDim.x * 1024;
   for (size_t x0 = (size_t)blockIdx.x * 1024 + threadIdx.x; x0 < nv; x0 += step) {  // 4 loads in flight
     msa_v4i v[4];
 #pragma unroll

@@ -129,11 +129,12 @@ class Plan:
 
     def run_info(self, stream=None) -> dict:
         """How the last run was computed (msa_plan_run_info): launch mode, chunks, whether every chunk of a
-        chunked banded run converged (else the exact launch recomputed the cells), warm-up stripes."""
+        chunked banded run converged (else the exact launch recomputed the cells), warm-up stripes, and whether
+        chunks >= 1 wrote int16 cells (widened by the add of the chunk constants)."""
         v = (C.c_int32 * 4)()
         LB.check(LB.lib().msa_plan_run_info(self._h, v, _stream_ptr(stream)), "msa_plan_run_info")
         return dict(mode={0: "stripe", 1: "flow", 2: "chunked"}[v[0]], chunks=int(v[1]), converged=int(v[2]),
-                    warm_stripes=int(v[3]))
+                    warm_stripes=int(v[3]) & 0xffff, int16_cells=(int(v[3]) >> 16) & 1)
 
     def launch_info(self) -> dict:
         """How the plan launches (msa_plan_launch_info): kernel mode, grid, threads, LDS bytes, flow pass-1

@@ -236,7 +236,8 @@ int msa_plan_results(msa_plan* plan, msa_pair_result* out, void* stream);
 /* How the last run was computed: out4 = {launch mode (0 stripe kernel, 1 two-pass
  * flow kernel, 2 chunked banded), chunks, converged (chunked: 1 = every chunk
  * converged and the cells came from the chunk launch, 0 = the exact single-mode
- * launch recomputed them; -1 otherwise), warm-up stripes per chunk}.
+ * launch recomputed them; -1 otherwise), warm-up stripes per chunk | 1 << 16 when
+ * chunks >= 1 wrote int16 cells widened by the chunk constants' add}.
  * Synchronizes `stream` for mode 2. */
 int msa_plan_run_info(msa_plan* plan, int32_t* out4, void* stream);
 /* How the plan launches (for tests and tools): out8 = {mode: 0 stripe_kernel (batch), 1 flow_kernel

@@ -4,6 +4,7 @@ Integer DP: every comparison is exact (scores, end cells, full H matrices,
 direction-derived tracebacks, node lists, stdout text)."""
 import hashlib
 import json
+import os
 
 import numpy as np
 import pytest
@@ -560,6 +561,8 @@ def test_c3_full_size(oracle, dev, LB):
     # the bench's pair converges in every chunk: the cells come from the chunked launch
     info = pl.run_info()
     assert info["mode"] == "chunked" and info["converged"] == 1 and info["chunks"] >= 4, info
+    # chunks >= 1 wrote int16 cells (in-band |H| well inside int16 here), widened by the constants' add
+    assert info["int16_cells"] == (0 if os.environ.get("MSA_BAND_H16") == "0" else 1), info
 
 
 @pytest.mark.parametrize("which", ["synthetic", "dissimilar"])
@@ -634,6 +637,7 @@ def test_banded_chunked(oracle, dev, LB, kind, m, w):
         info = pl.run_info()
         assert info["mode"] == "chunked" and info["chunks"] >= 4
         assert info["converged"] == (1 if kind == "similar" else 0), info
+        assert info["int16_cells"] == (0 if os.environ.get("MSA_BAND_H16") == "0" else 1), info
     assert pl.error() == 0
 
 
