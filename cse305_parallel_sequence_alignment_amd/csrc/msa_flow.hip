@@ -91,10 +91,6 @@ __device__ __forceinline__ void fl_poll_sleep(int polls) {
 #ifndef MSA_ABL
 #define MSA_ABL 0
 #endif
-// Gotoh pass 1 (R = 2): row 1 computes on tag-carrying values except at a phase's last step
-#ifndef FL_GOT_UNTAG
-#define FL_GOT_UNTAG 1
-#endif
 // v_max3_i32 as one opaque instruction: the compiler re-associates three max3 that share an operand
 // (h, R~, D~ of one cell) into a max + two max + a max3 -- four VALU instead of three
 __device__ __forceinline__ int vmax3(int a, int b, int c) {
@@ -886,7 +882,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
               const int uH = dpp_shr1(Z[kx >> 2][kx & 3], Zl2);
               const int uD = dpp_shr1(F[kx >> 2][kx & 3], Fo2);
               int h1, rr1, dd1;
-              if (kx == 15 || !FL_GOT_UNTAG) {
+              if (kx == 15) {  // row 1 on tag-carrying values only at a phase's last step (its hand-off)
                 const int t1 = (int)((unsigned)U | 3u) + sc;
                 const int t2p = (int)(((unsigned)E & ~3u) | 2u);
                 const int t3p = (int)(((unsigned)uD & ~3u) | 1u);

@@ -641,6 +641,34 @@ def test_banded_chunked(oracle, dev, LB, kind, m, w):
     assert pl.error() == 0
 
 
+@pytest.mark.parametrize("g,int16", [(50, 1), (60, 0)])
+def test_banded_chunked_int16_bound(oracle, dev, LB, g, int16):
+    """The int16 chunk cells' range bound (msa_plan_create: rows + h + g band <= 30,000): with g = 50 and band
+    512 the in-band cells reach -h - g band = -25,601 and stay int16 (cells written as int16, widened by the
+    add); g = 60 (30,720 past the bound) keeps int32 cells.  Either way score and every in-band cell equal
+    the banded oracle's."""
+    import torch
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+
+    rng = np.random.default_rng(g)
+    A, B = _similar(rng, 12000)
+    w = 512
+    if abs(len(A) - len(B)) > w:
+        B = B[:len(A) + w // 2]
+    pl = Plan(LB.NW_BANDED, LB.CELLS_H, [len(A)], [len(B)], [0], [0], match=1, mismatch=0, gap_open=g + 1,
+              gap_extend=g, band=w)
+    H = torch.empty(pl.cells_elems, dtype=torch.int32, device=dev)
+    score, digest = oracle.banded_ref(A, B, w, float(g), 1.0, want_digest=True)
+    pl.run(_dev(A, dev), _dev(B, dev), H)
+    assert pl.results()[0]["score"] == int(score)
+    assert pl.checksum(H) == digest
+    info = pl.run_info()
+    assert info["mode"] == "chunked" and info["chunks"] >= 4, info
+    if os.environ.get("MSA_BAND_H16") != "0":
+        assert info["int16_cells"] == int16, info
+    assert pl.error() == 0
+
+
 def _rescore(A, B, beg, cigar, ma, mi, go, ge):
     """Score of the local alignment a CIGAR describes from beg (1-based): affine gaps go + (k-1) ge."""
     import re
