@@ -522,8 +522,7 @@ __global__ __launch_bounds__((BK_W + 1) * 64) void band_kernel(KArgs a) {
       run_range(qa, qb, M3_{});
       run_range(qb, qc, M0_{});
       run_range(qc, P, M2_{});
-      lgkm_wait_aff<0>(ZA, FA, CAl, CAh);
-      lgkm_wait_aff<0>(ZB, FB, CBl, CBh);
+      lgkm_drain();
       if (k >= ks0 && lane == 0) {
         msa_stripe_meta* md = a.meta + pd.stripe0 + k;
         md->cs = cs;

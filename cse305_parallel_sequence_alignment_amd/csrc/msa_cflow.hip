@@ -437,8 +437,7 @@ __global__ __launch_bounds__((W + 1) * 64) __attribute__((amdgpu_waves_per_eu(CF
         }
         if (q < P) run_phase(q, INa, CWa, INb, CWb, T_{});
       }
-      lgkm_wait_v<0>(INa, CWa);
-      lgkm_wait_v<0>(INb, CWb);
+      lgkm_drain();
       if (stuck && lane == 0) atomicExch(a.err, 22);
       CF_STAMP(w, 1, __builtin_amdgcn_s_memrealtime());
 #ifdef MSA_STAMPS

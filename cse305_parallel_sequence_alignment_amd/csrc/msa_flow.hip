@@ -171,6 +171,11 @@ __device__ __forceinline__ void ds_reread_b128x4(unsigned a, fl_v4i (&in)[4]) {
 }
 template <int N = 0>
 __device__ __forceinline__ void lgkm_wait(int& v) { asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(v) : "i"(N) : "memory"); }
+// A stripe's end: every phase already waited for its prefetched inputs, so only the hand-off writes
+// may be in flight -- a plain wait, tying no registers.  (Tying the ring-input arrays here, as before,
+// kept the second buffer of the ping-pong live out of the phase loop, and the compiler then copied
+// every DPP input of the odd phases to a temporary: 32-40 extra v_mov per odd phase.)
+__device__ __forceinline__ void lgkm_drain() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 template <int N = 0>
 __device__ __forceinline__ void lgkm_wait_v(fl_v4i (&in)[4], fl_v4u& cw) {
   asm volatile("s_waitcnt lgkmcnt(%5)" : "+v"(in[0]), "+v"(in[1]), "+v"(in[2]), "+v"(in[3]), "+v"(cw) : "i"(N) : "memory");
@@ -1070,8 +1075,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
         if (q < P) run_phase(q, ZA, FA, CAl, CAh, ZB, FB, CBl, CBh, T_{}, F_{});
       }
       }
-      lgkm_wait_aff<0>(ZA, FA, CAl, CAh);
-      lgkm_wait_aff<0>(ZB, FB, CBl, CBh);
+      lgkm_drain();
       FL_STAMP(0, 1, __builtin_amdgcn_s_memrealtime());
       FL_STAMP(0, 2, (unsigned long long)nslow);
       msa_stripe_meta* md = a.meta + pd.stripe0 + k;
@@ -1315,8 +1319,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
         }
         if (q < P) run_phase(q, INa, CWa, INb, CWb, T_{});
       }
-      lgkm_wait_v<0>(INa, CWa);
-      lgkm_wait_v<0>(INb, CWb);
+      lgkm_drain();
       FL_STAMP(0, 1, __builtin_amdgcn_s_memrealtime());
       FL_STAMP(0, 2, (unsigned long long)nslow);
       FL_STAMP(1, 0, tw_in);
