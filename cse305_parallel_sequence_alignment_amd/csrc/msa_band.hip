@@ -401,8 +401,9 @@ __global__ __launch_bounds__((BK_W + 1) * 64) void band_kernel(KArgs a) {
       }
       // MODE bit 0: column jlo - 1 may fall in the phase; bit 1: column jhi + 1 (and the final cell)
       auto run_phase = [&](const int q, fl_v4i (&Zi)[4], fl_v4i (&Fi)[4], fl_v2u& Cl, fl_v2u& Ch, fl_v4i (&Zn)[4],
-                           fl_v4i (&Fn)[4], fl_v2u& Cln, fl_v2u& Chn, auto MODE_) __attribute__((always_inline)) {
+                           fl_v4i (&Fn)[4], fl_v2u& Cln, fl_v2u& Chn, auto MODE_, auto OUT_) __attribute__((always_inline)) {
         constexpr int MODE = decltype(MODE_)::value;
+        constexpr int OUT = decltype(OUT_)::value;  // 0: no cells (warm-up), 1: int32 cells, 2: int16 chunk cells
         const int need = Bin < 0 ? 0 : min(q + 1, Bin + 1) + dq_in;
         if (pubv < need) {
           wait_flag(need);
@@ -458,8 +459,8 @@ __global__ __launch_bounds__((BK_W + 1) * 64) void band_kernel(KArgs a) {
             ho[kx] = zn + (ctq - g * kx);
           }
 #ifndef BK_NOSTORE
-          if (outp) {
-            if (o16) {
+          if constexpr (OUT != 0) {
+            if constexpr (OUT == 2) {
               const fl_v2u hv = {__builtin_amdgcn_perm((unsigned)ho[4 * u + 1], (unsigned)ho[4 * u], 0x05040100u),
                                  __builtin_amdgcn_perm((unsigned)ho[4 * u + 3], (unsigned)ho[4 * u + 2], 0x05040100u)};
               if constexpr (MSA_H16_PAIRED) {
@@ -496,18 +497,16 @@ __global__ __launch_bounds__((BK_W + 1) * 64) void band_kernel(KArgs a) {
         }
         mask_in(q + 1, Zn, Fn);
       };
-      // phase q reads buffer A when q is even, B when odd (and prefetches into the other)
-      auto run_range = [&](int lo, int hi, auto M_) __attribute__((always_inline)) {
-        int q = lo;
-        if (q < hi && (q & 1)) {
-          run_phase(q, ZB, FB, CBl, CBh, ZA, FA, CAl, CAh, M_);
-          ++q;
+      // phase q reads buffer A when q is even, B when odd (and prefetches into the other).  Every range
+      // but the last starts and ends on an even phase (the boundaries below are rounded towards the more
+      // general edge mode), so a range is whole A/B pairs: at every range boundary buffer A is the
+      // current one and B is dead -- an odd-phase prologue / epilogue would keep both buffers live across
+      // the boundaries and make the compiler copy every DPP input of the B phases (32 v_mov per phase)
+      auto run_range = [&](int lo, int hi, auto M_, auto O_) __attribute__((always_inline)) {
+        for (int q = lo; q + 1 < hi; q += 2) {
+          run_phase(q, ZA, FA, CAl, CAh, ZB, FB, CBl, CBh, M_, O_);
+          run_phase(q + 1, ZB, FB, CBl, CBh, ZA, FA, CAl, CAh, M_, O_);
         }
-        for (; q + 1 < hi; q += 2) {
-          run_phase(q, ZA, FA, CAl, CAh, ZB, FB, CBl, CBh, M_);
-          run_phase(q + 1, ZB, FB, CBl, CBh, ZA, FA, CAl, CAh, M_);
-        }
-        if (q < hi) run_phase(q, ZA, FA, CAl, CAh, ZB, FB, CBl, CBh, M_);
       };
       using M0_ = std::integral_constant<int, 0>;
       using M1_ = std::integral_constant<int, 1>;
@@ -515,13 +514,27 @@ __global__ __launch_bounds__((BK_W + 1) * 64) void band_kernel(KArgs a) {
       using M3_ = std::integral_constant<int, 3>;
       // head [0, qa): left edges only; [qa, qb): both (a band too narrow for a clean middle);
       // middle [qb, qc): none; tail [qc, P): right edges and the final cell
-      const int qa = max(0, min(min(qlo, qhi), P));
-      const int qb = max(qa, min(qlo, P));
-      const int qc = max(qb, min(qhi, P));
-      run_range(0, qa, M1_{});
-      run_range(qa, qb, M3_{});
-      run_range(qb, qc, M0_{});
-      run_range(qc, P, M2_{});
+      const int qa0 = max(0, min(min(qlo, qhi), P));
+      const int qb0 = max(qa0, min(qlo, P));
+      const int qc0 = max(qb0, min(qhi, P));
+      // even boundaries within the even part Pe of [0, P), each rounded so that a phase moves only to a
+      // more general mode (both edges ⊇ left edges, none; right edges ⊇ none); an odd last phase runs
+      // with both edges
+      const int Pe = P & ~1;
+      const int qa = min(qa0 & ~1, Pe);
+      const int qb = min((qb0 + 1) & ~1, Pe);
+      const int qc = min(max(qb, qc0 & ~1), Pe);
+      // the cell stores' kind is the stripe's (uniform): one instantiation per kind, no branch per u-block
+      auto run_all = [&](auto O_) __attribute__((always_inline)) {
+        run_range(0, qa, M1_{}, O_);
+        run_range(qa, qb, M3_{}, O_);
+        run_range(qb, qc, M0_{}, O_);
+        run_range(qc, Pe, M2_{}, O_);
+        if (P & 1) run_phase(P - 1, ZA, FA, CAl, CAh, ZB, FB, CBl, CBh, M3_{}, O_);
+      };
+      if (!outp) run_all(std::integral_constant<int, 0>{});
+      else if (o16) run_all(std::integral_constant<int, 2>{});
+      else run_all(std::integral_constant<int, 1>{});
       lgkm_drain();
       if (k >= ks0 && lane == 0) {
         msa_stripe_meta* md = a.meta + pd.stripe0 + k;
