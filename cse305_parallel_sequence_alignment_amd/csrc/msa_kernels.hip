@@ -464,6 +464,8 @@ __device__ __forceinline__ unsigned step(const msa_kparams& kp, LaneState<ALG>& 
       // of G - g k in both halves; the phase's g (i + j) at its step 0 is subtracted once per phase
       // (run_phase), so no scalar arithmetic runs per step
       static_assert(TRACKPOS == 0, "packed pairs: score only");
+      // (KS = 16, unmasked: run_phase replaces this running max by a tree over the phase's carried
+      // values, and these updates are dead code there)
       L.pb = pk_max(L.pb, pk_add(nS[0], ct));
       hout = 0;
     } else if constexpr (swlin(ALG) || ALG == MSA_ALG_SWA) {
@@ -1280,7 +1282,19 @@ __global__ __launch_bounds__((W + 1 + (SGL ? 1 : 0)) * 64) void stripe_kernel(KA
                     make_int4((int)dirw[4 * h], (int)dirw[4 * h + 1], (int)dirw[4 * h + 2], (int)dirw[4 * h + 3]));
         }
         if constexpr (pk16(ALG)) {
-          // both pairs' H = G - g (i + j): the phase's best of G - g k, minus g (i + j) at its step 0
+          // both pairs' H = G - g (i + j): the phase's best of G - g k, minus g (i + j) at its step 0.
+          // KS = 16, unmasked: max over k of G_k - g k as a four-level tree over the carried values
+          // (independent ops, no serial chain of 16 dependent max with their wait states)
+          if constexpr (KS == 16 && !MASKED) {
+            int r8[8], r4[4], r2[2];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) r8[j] = pk_max(hist[0][2 * j], pk_add(hist[0][2 * j + 1], gkp[1]));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) r4[j] = pk_max(r8[2 * j], pk_add(r8[2 * j + 1], gkp[2]));
+#pragma unroll
+            for (int j = 0; j < 2; ++j) r2[j] = pk_max(r4[2 * j], pk_add(r4[2 * j + 1], gkp[4]));
+            L.pb = pk_max(r2[0], pk_add(r2[1], gkp[8]));
+          }
           L.best = pk_max(L.best, pk_add(L.pb, pk2(-(gdiag + kp.gap_open * KS * q))));
           L.pb = (int)0x80008000u;
         }
