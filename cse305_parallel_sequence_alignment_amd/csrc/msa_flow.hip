@@ -60,6 +60,8 @@ namespace msa {
 #ifndef FL_PS
 #define FL_PS 8         // phases per pass-2 segment (pass 1 saves its state every FL_PS phases)
 #endif
+// (a -DFL_PS=16 build produced wrong whole-sequence ref walks in round 5: only 8 is validated)
+static_assert(FL_PS == 8, "pass-2 segments are validated at 8 phases only");
 #define FL_P2INTS 576   // LDS ints per pass-2 wave: two value streams (256 each) + the block's codes (64)
 #define FL_FILLW 4      // waves per workgroup of the separate pass-2 launch (flow_fill_kernel)
 #define FL_SPIN_MAX (1u << 26)  // a spin limit sets err = the site's code (10..15) instead of hanging
