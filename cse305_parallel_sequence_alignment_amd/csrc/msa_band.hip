@@ -162,7 +162,10 @@ __global__ __launch_bounds__((BK_W + 1) * 64) void band_kernel(KArgs a) {
       unsigned long long* g_out = a.gbuf + (size_t)slot * 2 * a.gbuf_stride;
       int b = 0, ob = 0, consv = 0;
       unsigned spins = 0;
-      while (b <= Bmax || ob <= obmax) {
+      // (the loop's condition, progress counters and idle test are explicitly wave-uniform: with the
+      // phase code's per-kind instantiations the compiler turned this loop's back-edge exec-masked --
+      // tests/test_host.py::test_wait_loops_are_wave_uniform)
+      while (uni((b <= Bmax || ob <= obmax) ? 1 : 0)) {
         bool any = false;
         if (b <= Bmax) {
           int val[4], valf[4];
@@ -173,13 +176,16 @@ __global__ __launch_bounds__((BK_W + 1) * 64) void band_kernel(KArgs a) {
               const int col = cs0 + 16 * b + 64 * r + lane;
               // row 0: H(0,0) = 0, H(0,c) = -h - g c for 1 <= c <= band; the guessed row r0 > 0:
               // H = -h - g |c - r0| inside the band (the border's tent moved to the diagonal); F = -inf
-              int hv;
-              if (k0 == 0) hv = (col == 0) ? 0 : ((col >= 1 && col <= band) ? -hh - g * col : MSA_NEG);
-              else {
-                const int d = col > r0 ? col - r0 : r0 - col;
-                hv = (d <= band) ? -hh - g * d : MSA_NEG;
-              }
-              val[r] = (hv == MSA_NEG) ? MSA_NEG : hv + g * (r0 + col) - hh;  // Z = H~ - h
+              // (every lane computes both tents and selects: no lane-conditional block in the io
+              // loop, whose latch the compiler otherwise closes with an exec-mask branch)
+              const int d = col > r0 ? col - r0 : r0 - col;
+              int t0 = -hh - g * col, t1 = -hh - g * d;
+              asm("" : "+v"(t0), "+v"(t1));
+              const int hv = (k0 == 0) ? ((col == 0) ? 0 : ((col >= 1 && col <= band) ? t0 : MSA_NEG))
+                                       : ((d <= band) ? t1 : MSA_NEG);
+              int zv = hv + g * (r0 + col) - hh;  // Z = H~ - h
+              asm("" : "+v"(zv));
+              val[r] = (hv == MSA_NEG) ? MSA_NEG : zv;
               valf[r] = MSA_NEG;
             }
             nb = min(16, Bmax - b + 1);
@@ -221,7 +227,7 @@ __global__ __launch_bounds__((BK_W + 1) * 64) void band_kernel(KArgs a) {
             }
             FL_CBAR();
             if (lane == 0) lds_vstore(flags + 32, b + nb);
-            b += nb;
+            b = uni(b + nb);
             any = true;
           }
         }
@@ -251,13 +257,13 @@ __global__ __launch_bounds__((BK_W + 1) * 64) void band_kernel(KArgs a) {
                 }
               }
             }
-            ob += nb;
+            ob = uni(ob + nb);
             FL_CBAR();
             if (lane == 0) lds_vstore(flags + 64, ob);
             any = true;
           }
         }
-        if (!any) {
+        if (!uni(any ? 1 : 0)) {
           __builtin_amdgcn_s_sleep(FL_IOSLEEP);
           if (++spins > FL_SPIN_MAX) break;
         }
