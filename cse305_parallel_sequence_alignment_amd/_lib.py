@@ -83,6 +83,7 @@ def lib() -> C.CDLL:
     L.msa_partial_partition.argtypes = [P, P, sz, sz, sz, C.c_double, C.c_double, C.c_int, C.c_int, P, sz,
                                         C.POINTER(sz)]
     L.msa_partial_tables.argtypes = [P, P, sz, sz, C.c_double, C.c_double, C.c_int, C.c_int, P, P, P, P, P, P]
+    L.msa_partition_tables.argtypes = [P, P, P, P, P, P, sz, sz, sz, C.c_double, P, sz, C.POINTER(sz)]
     L.msa_non_parallel_tables.argtypes = [P, P, sz, sz, sz, sz, C.c_int, C.c_int, C.c_double, C.c_double, P, sz,
                                           C.POINTER(sz)]
     L.msa_subproblem_f64.argtypes = [P, P, sz, sz, sz, sz, C.c_int, C.c_double, C.c_double, C.c_int, P, P, P,
@@ -135,7 +136,7 @@ EXPORTED = [
     "msa_status_string", "msa_version", "msa_device_count", "msa_set_device_budget", "msa_device_budget_info", "msa_main_alignment", "msa_subproblem",
     "msa_non_parallel_tables", "msa_optimal_alignment", "msa_main_alignment_partitioned",
     "msa_subproblem_f64", "msa_subproblem_row",
-    "msa_partial_partition", "msa_partial_tables", "msa_plan_create", "msa_plan_destroy", "msa_plan_cells_size",
+    "msa_partial_partition", "msa_partial_tables", "msa_partition_tables", "msa_plan_create", "msa_plan_destroy", "msa_plan_cells_size",
     "msa_plan_run", "msa_plan_results", "msa_plan_error", "msa_plan_run_info", "msa_plan_clear_error", "msa_plan_scores",
     "msa_plan_stripe_meta", "msa_plan_stripes", "msa_plan_pair_layout", "msa_plan_launch_info",
     "msa_plan_checksum", "msa_plan_traceback", "msa_plan_traceback_gotoh",

@@ -863,10 +863,9 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   // chained through granules, claimed item-major -- for batches of fewer couples than two per CU whose code
   // rows fit LDS.  MSA_C4_KERNEL=lockstep / =cflow (diagnostics) force either kernel.
   if (kalg == MSA_ALG_SWLP && !single) {
-    static const bool lockstep = [] {
-      const char* e = std::getenv("MSA_C4_KERNEL");
-      return e && std::strcmp(e, "lockstep") == 0;
-    }();
+    // (read per plan, not cached: a test forces either kernel in one process)
+    const char* c4k = std::getenv("MSA_C4_KERNEL");
+    const bool lockstep = c4k && std::strcmp(c4k, "lockstep") == 0;
     int64_t nmax = 0, mmax = 0;
     for (int64_t p = 0; p < desc->n_pairs; ++p) {
       nmax = std::max(nmax, desc->n[p]);
@@ -878,10 +877,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     // workgroup hide each other's step latency): measured on C4's shape, 1,024 pairs 2.39 ms lock-step vs
     // 2.73 cflow; 512 pairs 2.07 vs 1.58, 128 pairs 0.72 vs 0.55 (profiles/r05_c4_*_bench.json)
     const int ncpl = (int)((desc->n_pairs + 1) / 2);
-    static const bool force_cflow = [] {
-      const char* e = std::getenv("MSA_C4_KERNEL");
-      return e && std::strcmp(e, "cflow") == 0;
-    }();
+    const bool force_cflow = c4k && std::strcmp(c4k, "cflow") == 0;
     if (!lockstep && clds <= 96 * 1024 && (force_cflow || ncpl < 2 * device_cus())) {
       P->cflow = true;
       P->fn = cflow_kernel<CF_W>;

@@ -81,6 +81,7 @@ __global__ __launch_bounds__((W + 1) * 64) __attribute__((amdgpu_waves_per_eu(CF
   // io-in: the code segment whose whole rows the LDS copies hold (C4's couples share one column
   // sequence: a workgroup loads it once, not per item -- ~2.5 us of an item's start)
   long long res_cod = -1;
+  int res_Yr = 0;  // bytes [0, res_Yr) of every copy's code row of segment res_cod are in LDS
 
   for (;;) {
     if (threadIdx.x == 0) flags[0] = atomicAdd(a.ticket, 1);
@@ -119,9 +120,10 @@ __global__ __launch_bounds__((W + 1) * 64) __attribute__((amdgpu_waves_per_eu(CF
       const int bmx = (kc < S) ? fl_bmax(kc, m, n) : -1;
       const int cs_o = fl_cs(kc);
       const uint8_t* gcod = a.cod + pd.cod_off;
-      // bytes [0, Yr) of every copy's code row are in LDS (all of them when the previous item of this
-      // workgroup had the same column segment)
-      int Yr = (pd.cod_off == res_cod) ? L8 : 0;
+      // bytes [0, Yr) of every copy's code row are in LDS: what the previous item of this workgroup
+      // loaded when it had the same column segment (carried, not assumed whole: an item loads only the
+      // prefix its blocks need)
+      int Yr = (pd.cod_off == res_cod) ? res_Yr : 0;
       res_cod = pd.cod_off;
       auto load_codes = [&](int Y1) __attribute__((always_inline)) {
         Y1 = min(Y1, L8);
@@ -236,6 +238,7 @@ __global__ __launch_bounds__((W + 1) * 64) __attribute__((amdgpu_waves_per_eu(CF
       }
       // (after the loop: a wave-uniform wait loop -- tests/test_host.py::test_wait_loops_are_wave_uniform)
       if ((b <= Bmax || bl <= bmx) && lane == 0) atomicExch(a.err, 20);
+      res_Yr = Yr;
     } else if (k0 + w < S) {
       // =================== compute wave: stripe k of the couple ===================
       const int k = k0 + w;
@@ -378,12 +381,14 @@ __global__ __launch_bounds__((W + 1) * 64) __attribute__((amdgpu_waves_per_eu(CF
             if (kx == FL_PF) issue_reads(q + 1, INn, CWn, pubn);  // prefetch phase q+1 (6 DS ops)
             // both pairs' score + 2g as int16: {s4 byte kk, 0, s4b byte kk, 0}
             const int s = (int)__builtin_amdgcn_perm(s4b, s4, 0x0c000c00u | ((4u + kk) << 16) | (unsigned)kk);
-            // diagonal and left first (no wait on this step's DPP), then the cell above: the DPP reads X
-            // three instructions after the previous step wrote it (its two wait states, no s_nop), and
-            // writes in place into the input register, whose lane 0 holds the row above (no copy)
+            // diagonal and left first (no wait on this step's DPP), then the cell above.  The DPP goes
+            // through the intrinsic, not inline asm: gfx950 needs 2 wait states between the VALU write
+            // of X and the DPP's read, and only the compiler's hazard recognizer pads (or schedules)
+            // for them -- round 5's asm DPP read X one instruction after the write at 47 sites
+            // (tests/test_host.py::test_dpp_reads_have_their_wait_states).  `old` = the ring value, so
+            // lane 0 takes the row above and the DPP writes in place (no copy: 113 VGPRs as before)
             const int dl = pk_max(pk_add(U, s), X);
-            int up = IN[u][kk];
-            asm volatile("v_mov_b32_dpp %0, %1 wave_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(up) : "v"(X));
+            const int up = dpp_shr1(IN[u][kk], X);
             X = pk_max(dl, up);
             U = up;
             xo[kx] = X;

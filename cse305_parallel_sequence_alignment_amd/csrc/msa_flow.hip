@@ -60,9 +60,18 @@ namespace msa {
 #ifndef FL_PS
 #define FL_PS 8         // phases per pass-2 segment (pass 1 saves its state every FL_PS phases)
 #endif
-// (a -DFL_PS=16 build produced wrong whole-sequence ref walks in round 5: only 8 is validated)
-static_assert(FL_PS == 8, "pass-2 segments are validated at 8 phases only");
-#define FL_P2INTS 576   // LDS ints per pass-2 wave: two value streams (256 each) + the block's codes (64)
+// A pass-2 wave's LDS area (p2_stage): two value streams of FL_P2VS ints (the row above the block's
+// 16 FL_PS columns), then the column codes its phases read, one staged dword per lane and round.
+// Lane r of phase k reads code dwords (63 - r + 16 k) / 4 + [0, 5), i.e. up to (63 + 16 (FL_PS - 1)) / 4
+// + 4: 48 dwords at FL_PS = 8, 80 at 16.  Round 5 staged a fixed 64 dwords, so a -DFL_PS=16 build read
+// its last phases' codes from the next wave's area (a wrong direction-byte plane, a wrong 97k walk
+// with the right score); the span now follows FL_PS.
+#define FL_P2VS (16 * FL_PS > 256 ? 16 * FL_PS : 256)  // ints per value stream
+#define FL_P2CODW ((63 + 16 * (FL_PS - 1)) / 4 + 5)     // code dwords a block's phases read
+#define FL_P2COD ((FL_P2CODW + 63) / 64 * 64)           // staged: whole rounds of 64 lanes
+#define FL_P2INTS (2 * FL_P2VS + FL_P2COD)              // 576 at FL_PS = 8 and 16
+static_assert(16 * FL_PS <= FL_P2VS, "a value stream holds the row above FL_PS phases of 16 columns");
+static_assert(FL_P2CODW <= FL_P2COD, "the staged code span covers every code dword the phases read");
 #define FL_FILLW 4      // waves per workgroup of the separate pass-2 launch (flow_fill_kernel)
 #define FL_SPIN_MAX (1u << 26)  // a spin limit sets err = the site's code (10..15) instead of hanging
 #ifndef FL_PF
@@ -1359,10 +1368,10 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
 }
 
 // A pass-2 block's inputs are staged in its wave's LDS area (FL_P2INTS ints) before the phase loop:
-// the row above its FL_PS phases, value stream k at lds + 256 k (columns [0, nv) from the bottom-row
+// the row above its FL_PS phases, value stream k at lds + FL_P2VS k (columns [0, nv) from the bottom-row
 // granules the caller loaded, row 0 for stripe 0, -inf past the producer's last block), and the column
-// codes the block reads -- columns cs - 63 + 16 q0 + [0, 256), one dword per lane from an aligned
-// staged copy -- at lds + 512.  The phase loop then issues no global load: a load in flight (codes
+// codes the block reads -- columns cs - 63 + 16 q0 + [0, 4 FL_P2COD), one dword per lane and round from
+// an aligned staged copy -- at lds + 2 FL_P2VS.  The phase loop then issues no global load: a load in flight (codes
 // prefetched phases ahead) made every phase wait for the previous phases' H / direction stores too --
 // one vmcnt counter for both -- i.e. ~1 us per phase.  2.3 KiB per wave: pass-2 workgroups fit beside
 // a pass-1 one on a CU.
@@ -1371,18 +1380,26 @@ __device__ __forceinline__ void p2_stage(lds_int* lds, int s, int nv, int ntot, 
                                          long long cod_copy, int cs, int q0) {
   const int b = cs - 63 + 16 * q0 - 1 + MSA_CPAD;  // byte of that first column in copy 0 (>= 0: CPAD 256)
   const int c = b & (MSA_NCOPY - 1);              // copy c holds it at the 16-aligned byte b - c
-  const unsigned w = *reinterpret_cast<const unsigned*>(cod + (size_t)c * cod_copy + (b - c) + 4 * lane);
+  unsigned w[FL_P2COD / 64];
+#pragma unroll
+  for (int d = 0; d < FL_P2COD / 64; ++d) {
+    // (round 0 stays inside the copy: b + 256 <= the padded row; later rounds -- FL_PS > 12 -- are clamped
+    // to it, the dwords past the row's end are never read by a phase < P)
+    const long long o = (b - c) + 4 * (64 * d + lane);
+    w[d] = *reinterpret_cast<const unsigned*>(cod + (size_t)c * cod_copy + (d == 0 ? o : min(o, cod_copy - 4)));
+  }
 #pragma unroll
   for (int k = 0; k < NV; ++k)
-    for (int v = (s == 0 ? 0 : nv) + lane; v < ntot; v += 64) *L(lds + 256 * k + v) = (s == 0) ? row0(v, k) : MSA_NEG;
-  *L(lds + 512 + lane) = (int)w;
+    for (int v = (s == 0 ? 0 : nv) + lane; v < ntot; v += 64) *L(lds + FL_P2VS * k + v) = (s == 0) ? row0(v, k) : MSA_NEG;
+#pragma unroll
+  for (int d = 0; d < FL_P2COD / 64; ++d) *L(lds + 2 * FL_P2VS + 64 * d + lane) = (int)w[d];
   FL_CBAR();  // (one wave's LDS ops execute in order: the phase loop's reads see these writes)
 }
 // Lane r's 16 column codes of the block's phase k (columns cs - r + 16 (q0 + k) + [0, 16)): five dwords
 // of the staged span and four byte-aligns (the shift (63 - r) mod 4 is the lane's for every phase).
 __device__ __forceinline__ fl_v4u p2_codes(lds_int* lds, int k, int lane) {
   const int o = (63 - lane) + 16 * k;
-  const lds_int* p = L(lds + 512 + (o >> 2));
+  const lds_int* p = L(lds + 2 * FL_P2VS + (o >> 2));
   const unsigned d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3], d4 = p[4];
   const unsigned sh = (unsigned)o & 3u;
   return fl_v4u{__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
@@ -1595,7 +1612,7 @@ __device__ __attribute__((noinline)) void fill_block_aff(kargs_c* ka, int blk, i
             const unsigned long long gz = gload(brz + 16 * q0 + v), gf = gload(brf + 16 * q0 + v);
             ok = ok && ((unsigned)(gz >> 32) == ep) && ((unsigned)(gf >> 32) == ep);
             *L(lds + v) = (int)(unsigned)gz;
-            *L(lds + 256 + v) = (int)(unsigned)gf;
+            *L(lds + FL_P2VS + v) = (int)(unsigned)gf;
           }
           ready = __ballot(!ok) == 0;
           if (!ready) __builtin_amdgcn_s_sleep(8);
@@ -1616,7 +1633,7 @@ __device__ __attribute__((noinline)) void fill_block_aff(kargs_c* ka, int blk, i
         int INZ[16], INF[16];
         {
           const lds_int4* srz = reinterpret_cast<const lds_int4*>(L(lds + 16 * (q - q0)));
-          const lds_int4* srf = reinterpret_cast<const lds_int4*>(L(lds + 256 + 16 * (q - q0)));
+          const lds_int4* srf = reinterpret_cast<const lds_int4*>(L(lds + FL_P2VS + 16 * (q - q0)));
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const fl_v4i vz = srz[u], vf = srf[u];
@@ -1727,7 +1744,7 @@ __device__ __attribute__((noinline)) void fill_block_aff2(kargs_c* ka, int blk, 
             const unsigned long long gz = gload(brz + 16 * q0 + v), gf = gload(brf + 16 * q0 + v);
             ok = ok && ((unsigned)(gz >> 32) == ep) && ((unsigned)(gf >> 32) == ep);
             *L(lds + v) = (int)(unsigned)gz;
-            *L(lds + 256 + v) = (int)(unsigned)gf;
+            *L(lds + FL_P2VS + v) = (int)(unsigned)gf;
           }
           ready = __ballot(!ok) == 0;
           if (!ready) __builtin_amdgcn_s_sleep(8);
@@ -1748,7 +1765,7 @@ __device__ __attribute__((noinline)) void fill_block_aff2(kargs_c* ka, int blk, 
         int INZ[16], INF[16];
         {
           const lds_int4* srz = reinterpret_cast<const lds_int4*>(L(lds + 16 * (q - q0)));
-          const lds_int4* srf = reinterpret_cast<const lds_int4*>(L(lds + 256 + 16 * (q - q0)));
+          const lds_int4* srf = reinterpret_cast<const lds_int4*>(L(lds + FL_P2VS + 16 * (q - q0)));
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const fl_v4i vz = srz[u], vf = srf[u];
@@ -1882,7 +1899,7 @@ __device__ __attribute__((noinline)) void fill_block_got(kargs_c* ka, int blk, i
             const unsigned long long gz = gload(brz + 16 * q0 + v), gf = gload(brf + 16 * q0 + v);
             ok = ok && ((unsigned)(gz >> 32) == ep) && ((unsigned)(gf >> 32) == ep);
             *L(lds + v) = (int)(unsigned)gz;
-            *L(lds + 256 + v) = (int)(unsigned)gf;
+            *L(lds + FL_P2VS + v) = (int)(unsigned)gf;
           }
           ready = __ballot(!ok) == 0;
           if (!ready) __builtin_amdgcn_s_sleep(8);
@@ -1912,7 +1929,7 @@ __device__ __attribute__((noinline)) void fill_block_got(kargs_c* ka, int blk, i
         int INZ[16], INF[16];
         {
           const lds_int4* srz = reinterpret_cast<const lds_int4*>(L(lds + 16 * (q - q0)));
-          const lds_int4* srf = reinterpret_cast<const lds_int4*>(L(lds + 256 + 16 * (q - q0)));
+          const lds_int4* srf = reinterpret_cast<const lds_int4*>(L(lds + FL_P2VS + 16 * (q - q0)));
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const fl_v4i vz = srz[u], vf = srf[u];
@@ -2045,7 +2062,7 @@ __device__ __attribute__((noinline)) void fill_block_got2(kargs_c* ka, int blk, 
             const unsigned long long gz = gload(brz + 16 * q0 + v), gf = gload(brf + 16 * q0 + v);
             ok = ok && ((unsigned)(gz >> 32) == ep) && ((unsigned)(gf >> 32) == ep);
             *L(lds + v) = (int)(unsigned)gz;
-            *L(lds + 256 + v) = (int)(unsigned)gf + h4;
+            *L(lds + FL_P2VS + v) = (int)(unsigned)gf + h4;
           }
           ready = __ballot(!ok) == 0;
           if (!ready) __builtin_amdgcn_s_sleep(8);
@@ -2074,7 +2091,7 @@ __device__ __attribute__((noinline)) void fill_block_got2(kargs_c* ka, int blk, 
         int INZ[16], INF[16];
         {
           const lds_int4* srz = reinterpret_cast<const lds_int4*>(L(lds + 16 * (q - q0)));
-          const lds_int4* srf = reinterpret_cast<const lds_int4*>(L(lds + 256 + 16 * (q - q0)));
+          const lds_int4* srf = reinterpret_cast<const lds_int4*>(L(lds + FL_P2VS + 16 * (q - q0)));
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const fl_v4i vz = srz[u], vf = srf[u];

@@ -1742,7 +1742,9 @@ namespace msa {
 // wins (the reference's strict '>').  Key = (val ^ 0x80000000) << 32 |
 // (~scan_idx & 0x3fffffff) << 2 | type, reduced with 64-bit atomicMax.
 // Forward planes F* and reverse planes R' (reverse fill = forward fill of the
-// reversed strings) are read in the skewed stripe layout.
+// reversed strings) are read in the skewed stripe layout (msa_partial_partition), or
+// the six tables row-major as the caller of findPartitionParallel holds them
+// (msa_partition_tables).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int skew_get(const int32_t* plane, const msa_pair_desc& pd, const msa_stripe_meta* meta,
                                         int i, int j) {
@@ -1752,12 +1754,30 @@ __device__ __forceinline__ int skew_get(const int32_t* plane, const msa_pair_des
   return plane[e];
 }
 
-__global__ void partition_kernel(const int32_t* F1, const int32_t* F2, const int32_t* F3, const int32_t* R1,
-                                 const int32_t* R2, const int32_t* R3, const msa_pair_desc* pdf,
-                                 const msa_pair_desc* pdr, const msa_stripe_meta* mf, const msa_stripe_meta* mr,
-                                 int p, int hh, unsigned long long* keys) {
-  const msa_pair_desc f = pdf[0], rv = pdr[0];
-  const int m = f.m, n = f.n;
+// row-major tables as the reference holds them (findPartitionParallel's own inputs, host
+// vector<vector<int>> flattened): T* (m+1) x (n+1), TR* (m+2) x (n+2), TR[i][j] at (m+1-i', n+1-j')
+struct PartSkew {
+  const int32_t *F1, *F2, *F3, *R1, *R2, *R3;
+  const msa_pair_desc *pdf, *pdr;
+  const msa_stripe_meta *mf, *mr;
+  __device__ void get(int m, int n, int i, int j, int f[3], int r[3]) const {
+    const msa_pair_desc f0 = pdf[0], r0 = pdr[0];
+    f[0] = skew_get(F1, f0, mf, i, j), f[1] = skew_get(F2, f0, mf, i, j), f[2] = skew_get(F3, f0, mf, i, j);
+    const int ri = m + 1 - i, rj = n + 1 - j;  // reverse fill = forward fill of the reversed strings
+    r[0] = skew_get(R1, r0, mr, ri, rj), r[1] = skew_get(R2, r0, mr, ri, rj), r[2] = skew_get(R3, r0, mr, ri, rj);
+  }
+};
+struct PartRowMajor {
+  const int32_t *F1, *F2, *F3, *R1, *R2, *R3;
+  __device__ void get(int m, int n, int i, int j, int f[3], int r[3]) const {
+    const size_t ef = (size_t)i * (n + 1) + j, er = (size_t)i * (n + 2) + j;
+    f[0] = F1[ef], f[1] = F2[ef], f[2] = F3[ef];
+    r[0] = R1[er], r[1] = R2[er], r[2] = R3[er];
+  }
+};
+
+template <class TABS>
+__global__ void partition_kernel(TABS tabs, int m, int n, int p, int hh, unsigned long long* keys) {
   const int bm = m / p, bn = n / p;
   const long long rowcells = (long long)bm * n, colcells = (long long)bn * m;
   const long long total = (long long)(p - 1) * (rowcells + colcells);
@@ -1784,12 +1804,11 @@ __global__ void partition_kernel(const int32_t* F1, const int32_t* F2, const int
       if (j > n) continue;
       slot = 2 * k + 1;
     }
-    const int f1 = skew_get(F1, f, mf, i, j), f2 = skew_get(F2, f, mf, i, j), f3 = skew_get(F3, f, mf, i, j);
-    const int ri = m + 1 - i, rj = n + 1 - j;
-    const int r1 = skew_get(R1, rv, mr, ri, rj), r2 = skew_get(R2, rv, mr, ri, rj), r3 = skew_get(R3, rv, mr, ri, rj);
-    const int val = imax3(wrap_add(f1, r1), wrap_add(wrap_add(f2, r2), hh), wrap_add(wrap_add(f3, r3), hh));
+    int f[3], r[3];
+    tabs.get(m, n, i, j, f, r);
+    const int val = imax3(wrap_add(f[0], r[0]), wrap_add(wrap_add(f[1], r[1]), hh), wrap_add(wrap_add(f[2], r[2]), hh));
     if (val == INT32_MIN) continue;  // can never beat the reference's INT_MIN start
-    const unsigned type = (unsigned)firstmax3(f1, f2, f3);
+    const unsigned type = (unsigned)firstmax3(f[0], f[1], f[2]);
     const unsigned long long key = ((unsigned long long)((unsigned)val ^ 0x80000000u) << 32) |
                                    ((unsigned long long)((~(unsigned)idx) & 0x3fffffffu) << 2) | type;
     if (slot != cur_slot) {

@@ -25,6 +25,7 @@
  *                        partition step (main_alignment.cpp:365,372) enabled
  *   msa_partial_tables   initializeTables/initializeReverseTables/fillTablesParallel/
  *                        fillReverseTablesParallel, partial.h:25-35, partial.cpp:13-79
+ *   msa_partition_tables findPartitionParallel over caller tables, partial.h:37-39, partial.cpp:81-146
  *   msa_plan_*           device-resident batch / single-pair fills (build extension:
  *                        configs C2-C5 of BASELINE.json; no reference counterpart,
  *                        same cell recurrence family as subproblem_alignment.cpp:396-398)
@@ -175,6 +176,15 @@ int msa_partial_partition(const char* A0, const char* B0, size_t m, size_t n, si
  * row-major; any pointer may be NULL. */
 int msa_partial_tables(const char* A0, const char* B0, size_t m, size_t n, double g, double h, int start_type,
                        int end_type, int32_t* T1, int32_t* T2, int32_t* T3, int32_t* R1, int32_t* R2, int32_t* R3);
+
+/* findPartitionParallel(T1, T2, T3, TR1, TR2, TR3, m, n, p, h) (partial.h:37-39,
+ * partial.cpp:81-146) over tables the caller already holds: T* (m+1)x(n+1) and
+ * TR* (m+2)x(n+2) int32, row-major, as partial.cpp's own fills leave them.  The
+ * band maxima run on the GPU (int32 wrap, first maximum in the reference's scan
+ * order); out receives the p+1 points sorted as partial.cpp:141-143. */
+int msa_partition_tables(const int32_t* T1, const int32_t* T2, const int32_t* T3, const int32_t* R1,
+                         const int32_t* R2, const int32_t* R3, size_t m, size_t n, size_t p, double h,
+                         msa_node* out, size_t cap, size_t* n_out);
 
 /* ---- device-resident plans (configs C2-C5) --------------------------------
  * A plan owns the device scratch for one shape of work; running it launches

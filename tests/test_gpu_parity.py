@@ -178,13 +178,21 @@ def test_sw_linear_c4_shape_scores(oracle, dev, LB):
         assert res[k]["score"] == oracle.sw(As[k], B, 1, 0, 1, 1)["score"]
 
 
+# the two kernels a packed score-only batch can run (msa_capi.hip, MSA_C4_KERNEL read per plan): cflow_kernel
+# (the default below two couples per CU) and the lock-step stripe kernel (batch or split mode)
+C4_KERNELS = {"cflow": ("cflow",), "lockstep": ("stripe", "split")}
+
+
+@pytest.mark.parametrize("c4_kernel", sorted(C4_KERNELS))
 @pytest.mark.parametrize("scoring", [(1, 0, 1), (2, 1, 1), (3, 0, 2), (5, 2, 3)])
-def test_sw_linear_packed_pairs(oracle, dev, LB, scoring):
+def test_sw_linear_packed_pairs(oracle, dev, LB, scoring, c4_kernel, monkeypatch):
     """Score-only batches whose pair couples (2c, 2c+1) share sizes and column sequence run two pairs per lane
     as packed int16 (MSA_ALG_SWLP): every score equals the oracle's -- couples of different shapes in one plan,
-    an odd pair count (the last couple repeats its pair), similar and random pairs, sizes from 1 to 2,000."""
+    an odd pair count (the last couple repeats its pair), similar and random pairs, sizes from 1 to 2,000 --
+    on both kernels (the launch mode is asserted)."""
     from cse305_parallel_sequence_alignment_amd.plan import Plan
 
+    monkeypatch.setenv("MSA_C4_KERNEL", c4_kernel)
     ma, mi, g = scoring
     rng = np.random.default_rng(40 + ma)
     shapes = [(700, 650), (700, 650), (64, 64), (64, 64), (1, 9), (1, 9), (2000, 1999), (2000, 1999), (130, 7),
@@ -203,6 +211,7 @@ def test_sw_linear_packed_pairs(oracle, dev, LB, scoring):
         bo.append(Bs[c][0])
     pl = Plan(LB.SW_LINEAR, LB.CELLS_NONE, [m for m, _ in shapes], [n for _, n in shapes], ao, bo, match=ma,
               mismatch=mi, gap_open=g, gap_extend=g, single=False)
+    assert pl.launch_info()["mode"] in C4_KERNELS[c4_kernel]
     pl.run(_dev(b"".join(As), dev), _dev(Bcat, dev))
     res = pl.results()
     for k, (m, n) in enumerate(shapes):
@@ -210,21 +219,25 @@ def test_sw_linear_packed_pairs(oracle, dev, LB, scoring):
         assert res[k]["score"] == oracle.sw(As[k], B, ma, mi, g, g)["score"], (k, m, n)
 
 
-@pytest.mark.parametrize("kind", ["packed", "int32_H", "affine_dir"])
-def test_batch_split_pairs(oracle, dev, LB, kind):
-    """A batch with fewer pairs than two workgroups per CU splits every pair into items of W stripes chained
-    through granules (kp.single == 3, the per-rank share of C4 at 8 GPUs): scores (and for the int32 plan the
-    full H matrices, for SW affine the device traceback) equal the oracle's."""
+@pytest.mark.parametrize("kind", ["packed", "packed_lockstep", "int32_H", "affine_dir"])
+def test_batch_split_pairs(oracle, dev, LB, kind, monkeypatch):
+    """A batch with fewer pairs than two workgroups per CU splits every pair into items chained through
+    granules: packed couples run cflow_kernel by default (items of 4 stripes) and the lock-step kernel's split
+    mode when forced (kp.single == 3, as every unpacked batch here); scores (and for the int32 plan the full H
+    matrices, for SW affine the device traceback) equal the oracle's."""
     import torch
     from cse305_parallel_sequence_alignment_amd.plan import Plan
 
-    rng = np.random.default_rng({"packed": 1, "int32_H": 2, "affine_dir": 3}[kind])
-    if kind == "packed":
+    rng = np.random.default_rng({"packed": 1, "packed_lockstep": 1, "int32_H": 2, "affine_dir": 3}[kind])
+    if kind.startswith("packed"):
+        if kind == "packed_lockstep":
+            monkeypatch.setenv("MSA_C4_KERNEL", "lockstep")
         K, m, n = 37, 1500, 1400  # odd count: the last couple repeats its pair
         As = [rs(rng, m) for _ in range(K)]
         B = rs(rng, n)
         pl = Plan(LB.SW_LINEAR, LB.CELLS_NONE, [m] * K, [n] * K, [k * m for k in range(K)], [0] * K, match=1,
                   mismatch=0, gap_open=1, gap_extend=1, single=False)
+        assert pl.launch_info()["mode"] == ("cflow" if kind == "packed" else "split")
         pl.run(_dev(b"".join(As), dev), _dev(B, dev))
         res = pl.results()
         for k in range(K):
@@ -432,7 +445,35 @@ def test_c4_full_batch_scores(dev, LB):
     assert d.cpu().tolist() == want
 
 
-@pytest.mark.parametrize("m,n,w", [(300, 290, 32), (1000, 1000, 64), (1500, 1490, 512), (700, 700, 1)])
+@pytest.mark.parametrize("world,rank", [(8, 0), (8, 7), (4, 3), (2, 1)])
+def test_c4_rank_share_scores(dev, LB, world, rank):
+    """The C4 share one rank of an N-GPU run aligns (shard.ShardedBatch's contiguous block: 128 pairs at 8
+    GPUs, 256 at 4, 512 at 2) runs cflow_kernel, as bench.py's multi-GPU C4 does: every score of the share,
+    over three launches of one plan (epochs), equals its slice of tests/golden/c4_scores.json."""
+    import torch
+    from cse305_parallel_sequence_alignment_amd import data
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+    from cse305_parallel_sequence_alignment_amd.shard import shard_range
+
+    want = json.loads((GOLDEN / "c4_scores.json").read_text())["scores"]
+    L = data.C4_LEN
+    lo, hi = shard_range(data.C4_PAIRS, rank, world)
+    assert hi - lo == data.C4_PAIRS // world
+    K = hi - lo
+    pl = Plan(LB.SW_LINEAR, LB.CELLS_NONE, [L] * K, [L] * K, [k * L for k in range(K)], [0] * K, match=1,
+              mismatch=0, gap_open=1, gap_extend=1)
+    assert pl.launch_info()["mode"] == "cflow"
+    dq, dr = _dev(b"".join(data.c4_queries(lo, hi)), dev), _dev(data.c4_reference(), dev)
+    d = torch.empty(K, dtype=torch.int32, device=dev)
+    for _ in range(3):
+        d.fill_(-1)
+        pl.run(dq, dr)
+        pl.scores_into(d)
+        assert d.cpu().tolist() == want[lo:hi]
+    assert pl.error() == 0
+
+
+@pytest.mark.parametrize("m,n,w",[(300, 290, 32), (1000, 1000, 64), (1500, 1490, 512), (700, 700, 1)])
 def test_nw_banded_reference_gotoh(oracle, dev, LB, m, n, w):
     """C3's kernel (banded reference Gotoh, g=1 h=2) at small sizes: every in-band H cell and the score."""
     import torch

@@ -375,3 +375,103 @@ def test_harness_drivers(oracle, dev, dataset, tmp_path):
     assert H.test_n_cores_thread(names, seqs, test_pairs=6, threads=3, csv_path=str(tmp_path / "nc.csv"),
                                  max_len=200, out=io.StringIO()) == 0
     assert len((tmp_path / "nc.csv").read_text().splitlines()) == 8
+
+
+# ---- the reference's main_alignment.h and partial.h through libmsa_compat.so (C++ drop-ins) ----
+
+OPT_DRIVERS = {"compat_header": ROOT / "tests" / "cpp" / "optimal_driver",
+               "reference_header": ROOT / "oracle" / "_ref" / "optimal_driver_refhdr"}
+PART_DRIVERS = {"compat_header": ROOT / "tests" / "cpp" / "partial_driver",
+                "reference_header": ROOT / "oracle" / "_ref" / "partial_driver_refhdr"}
+PROGRESS = "bp1\nbp1.2\nbp2\nbp3\nbp4\n"
+
+
+def _driver(drivers, which):
+    drv = drivers[which]
+    if not drv.exists():
+        pytest.skip(f"{drv.name} not built (needs /root/reference at build time)")
+    return drv
+
+
+def _bp_args(bp):
+    return f"{len(bp)} " + " ".join(f"{i} {j} {t}" for i, j, t in bp)
+
+
+def _sched_expect(bp, m, n, p):
+    """main_alignment.cpp:158-200 restated: omega per subproblem, its inclusive prefix sum, and
+    assign_processors as optimal_alignment calls it (:244-249)."""
+    import math
+
+    omega = [max(math.ceil((b[0] - a[0]) / (m / p)), math.ceil((b[1] - a[1]) / (n / p))) for a, b in zip(bp, bp[1:])]
+    sums = list(np.cumsum(omega))
+
+    def assign(prev, cur):
+        r = prev % 3
+        return (cur + 2) // 3 if r == 0 else (1 + cur // 3 if r == 1 else 1 + (cur + 1) // 3)
+
+    procs = [assign(0, omega[0])] + [assign(sums[k - 1], omega[k]) for k in range(1, len(omega))]
+    return omega, [int(x) for x in sums], procs
+
+
+@pytest.mark.parametrize("which", list(OPT_DRIVERS))
+def test_cpp_main_alignment_api(dev, which):
+    """alignment_algorithm/main_alignment.h's API from C++ (the driver compiled against the build's header,
+    and against the reference's own unmodified main_alignment.h), linked against libmsa_compat.so:
+    optimal_alignment's stdout for all 77 partitions of tests/golden/optimal.json (every node
+    reference-produced); OptimalAlignmentMapThread + print_align on the 41 reference-produced Subproblem
+    paths; the scheduler helpers (omega, ParallelPrefix, assign_processors, the block bodies)."""
+    drv = _driver(OPT_DRIVERS, which)
+    lines, want = [], []
+    for c in OPT:
+        A, B = c["A"], c["B"]
+        lines.append(f"opt {c['g']!r} {c['h']!r} 4 {len(A)} {len(B)} {A} {B} {_bp_args(c['bp'])}\n")
+        want.append(c["ref"]["text"])
+    paths = json.loads((GOLDEN / "subproblem_paths.json").read_text())
+    for c in paths:
+        A, B = c["A"], c["B"]
+        lines.append(f"map {c['g']!r} {c['h']!r} 3 {c['start']} {c['end']} 0 0 {len(A)} {len(B)} {A} {B}\n")
+        want.append(PROGRESS + "".join(f"({i}, {j}, {t})\n" for i, j, t in c["nodes"]) +
+                    "END %d %d %d\n" % tuple(c["end_node"]))
+    for c in OPT[::7]:
+        m, n = len(c["A"]), len(c["B"])
+        for p in (1, 3, 4, 8):
+            bp = c["bp"]
+            omega, sums, procs = _sched_expect(bp, m, n, p)
+            lines.append(f"sched {p} {m} {n} {_bp_args(bp)}\n")
+            init = list(np.cumsum(omega))
+            want.append("OMEGA " + " ".join(map(str, omega)) + "\nSUMS " + " ".join(map(str, sums)) +
+                        "\nPROCS " + " ".join(map(str, procs)) + "\nOMEGA1 " + " ".join(map(str, omega)) +
+                        "\nINIT " + " ".join(str(int(x)) for x in init) + f" | {int(init[-1])}\n" +
+                        "ADD7 " + " ".join(str(int(x) + 7) for x in init) + "\n")
+    outs = _run_driver(drv, lines)
+    for ln, got, exp in zip(lines, outs, want):
+        assert got == exp, (ln[:120], got[-300:], exp[-300:])
+
+
+@pytest.mark.parametrize("which", list(PART_DRIVERS))
+def test_cpp_partial_api(oracle, dev, which):
+    """sequence_alignment/partial.h's API from C++ (the driver compiled against the build's header, and
+    against the reference's own unmodified partial.h), linked against libmsa_compat.so: every partition
+    of partial.json (80) and partial_ties.json (116, the std::sort tie order), both through
+    findPartialBalancedPartitionParallel and through the step API (initialize*, fill*Parallel,
+    findPartitionParallel over the caller's tables); the six filled tables against the oracle's
+    restatement (pinned to the reference's partial.cpp); score()."""
+    drv = _driver(PART_DRIVERS, which)
+    cases = json.loads((GOLDEN / "partial.json").read_text()) + json.loads((GOLDEN / "partial_ties.json").read_text())
+    lines, want = [], []
+    for c in cases:
+        lines.append(f"part {c['p']} {c['g']!r} {c['h']!r} {c['start']} {c['end']} {c['A']} {c['B']}\n")
+        pts = " ".join(f"{i} {j} {t}" for i, j, t in c["partition"])
+        want.append(f"PART {pts}\nSTEP {pts}\n")
+    tab_cases = [c for c in cases[:80:9]]
+    for c in tab_cases:
+        lines.append(f"tabs {c['g']!r} {c['h']!r} {c['start']} {c['end']} {c['A']} {c['B']}\n")
+        T, R = oracle.partial_tables(c["A"].encode(), c["B"].encode(), c["g"], c["h"], c["start"], c["end"])
+        want.append("".join(f"{nm}\n" + "".join("".join(f"{int(x)} " for x in row) + "\n" for row in tab)
+                            for nm, tab in zip(("T1", "T2", "T3", "TR1", "TR2", "TR3"), T + R)))
+    for a, b in (("A", "A"), ("A", "C"), ("G", "T"), ("T", "T")):
+        lines.append(f"score {a} {b}\n")
+        want.append(f"SCORE {0 if a == b else 1}\n")
+    outs = _run_driver(drv, lines)
+    for ln, got, exp in zip(lines, outs, want):
+        assert got == exp, (ln[:120], got[:300], exp[:300])

@@ -1,6 +1,7 @@
 """Host-side logic on CPU: the C-ABI library, stripe geometry, SW oracle vs brute force."""
 import ctypes as C
 import re
+import sys
 
 import numpy as np
 import pytest
@@ -167,6 +168,69 @@ def test_compat_library_exports_subproblem_members():
     assert (ROOT / "tests" / "cpp" / "subproblem_driver").exists(), "make -C tests/cpp"
 
 
+# main_alignment.h:17-38 and partial.h:23-41 with the reference's C++ manglings (types as declared by the
+# reference headers; `align` is struct alignment_point, queue_indices struct parallel_prefix_queue_element)
+MAIN_ALIGNMENT_SYMBOLS = [
+    "_Z25OptimalAlignmentMapThreadPcS_mmmmmiiddRP15alignment_pointS2_", "_Z11print_alignP15alignment_point",
+    "_Z18PrefixSumMapThreadRSt6vectorIlSaIlEElP29parallel_prefix_queue_element",
+    "_Z19PrefixInitMapThreadRSt6vectorIlSaIlEES2_R29parallel_prefix_queue_element",
+    "_Z14ParallelPrefixmRSt6vectorIlSaIlEES2_",
+    "_Z21ComputeOmegaMapThreadN9__gnu_cxx17__normal_iteratorIP15alignment_pointSt6vectorIS1_SaIS1_EEEES6_mmmRS3_IlSaIlEEl",
+    "_Z22compute_omega_parallelRSt6vectorI15alignment_pointSaIS0_EEmmmmRS_IlSaIlEE", "_Z17assign_processorsll",
+    "_Z17optimal_alignmentPcS_St6vectorI15alignment_pointSaIS1_EEmmmdd", "_Z23main_alignment_functionPcS_mmmdd",
+]
+PARTIAL_SYMBOLS = [
+    "_Z5scorecc", "_Z16initializeTablesRSt6vectorIS_IiSaIiEESaIS1_EES4_S4_mmddi",
+    "_Z23initializeReverseTablesRSt6vectorIS_IiSaIiEESaIS1_EES4_S4_mmddi",
+    "_Z18fillTablesParallelPKcS0_mmRSt6vectorIS1_IiSaIiEESaIS3_EES6_S6_ddm",
+    "_Z25fillReverseTablesParallelPKcS0_mmRSt6vectorIS1_IiSaIiEESaIS3_EES6_S6_ddm",
+    "_Z21findPartitionParallelRKSt6vectorIS_IiSaIiEESaIS1_EES5_S5_S5_S5_S5_mmmd",
+    "_Z36findPartialBalancedPartitionParallelPKcS0_mmmddiiRSt6vectorI15alignment_pointSaIS2_EE",
+]
+
+
+def test_compat_library_exports_main_alignment_and_partial_api():
+    """libmsa_compat.so defines every function alignment_algorithm/main_alignment.h:17-38 and
+    sequence_alignment/partial.h:23-41 declare (extractPartitions aside: the reference defines no body),
+    with the reference's C++ manglings; the drivers compiled against the reference's own headers
+    (oracle/_ref/*_driver_refhdr, where /root/reference exists) linked against it."""
+    lib = ROOT / "cse305_parallel_sequence_alignment_amd" / "libmsa_compat.so"
+    L = C.CDLL(str(lib))
+    for sym in MAIN_ALIGNMENT_SYMBOLS + PARTIAL_SYMBOLS:
+        assert hasattr(L, sym), sym
+    for d in ("optimal_driver", "partial_driver"):
+        assert (ROOT / "tests" / "cpp" / d).exists(), "make -C tests/cpp"
+
+
+def _drivers(name):
+    out = [ROOT / "tests" / "cpp" / name]
+    ref = ROOT / "oracle" / "_ref" / f"{name}_refhdr"
+    return out + ([ref] if ref.exists() else [])
+
+
+def test_cpp_scheduler_helpers_and_score_on_host():
+    """The host-only parts of the two C++ APIs through both driver builds (no GPU needed): the scheduler
+    bookkeeping of main_alignment.cpp:158-200 (omega, ParallelPrefix, assign_processors, the block bodies)
+    and partial.cpp:9-11's score; a GPU entry point without a GPU throws (no CPU fallback)."""
+    import subprocess
+
+    cases = "sched 4 40 40 5 0 0 -1 1 13 3 1 23 3 40 37 1 40 40 1\nsched 3 10 7 3 0 0 -1 4 2 2 10 7 1\n" \
+            "opt 1.0 2.0 4 4 5 AGGA AGTGC 2 0 0 -1 4 5 1\n"
+    want = ("OMEGA 2 1 4 1\nSUMS 2 3 7 8\nPROCS 1 1 2 1\nOMEGA1 2 1 4 1\nINIT 2 3 7 8 | 8\nADD7 9 10 14 15\nEND_CASE\n"
+            # (4,2): ceil(4/(10/3)) = 2, ceil(2/(7/3)) = 1; (6,5): ceil(1.8) = 2, ceil(2.14) = 3
+            "OMEGA 2 3\nSUMS 2 5\nPROCS 1 2\nOMEGA1 2 3\nINIT 2 5 | 5\nADD7 9 12\nEND_CASE\n")
+    for drv in _drivers("optimal_driver"):
+        r = subprocess.run([str(drv)], input=cases, capture_output=True, text=True, timeout=60)
+        assert r.returncode == 0, r.stderr
+        assert r.stdout.startswith(want), (drv.name, r.stdout)
+        assert "ERROR optimal_alignment: no gfx950 device" in r.stdout or "ERROR" not in r.stdout
+    for drv in _drivers("partial_driver"):
+        r = subprocess.run([str(drv)], input="score A A\nscore A C\nscore T G\n", capture_output=True, text=True,
+                           timeout=60)
+        assert r.returncode == 0, r.stderr
+        assert r.stdout == "SCORE 0\nEND_CASE\nSCORE 1\nEND_CASE\nSCORE 1\nEND_CASE\n", drv.name
+
+
 def _similarity_reference_loop(s1: bytes, s2: bytes, T: int) -> float:
     """pull_data.cpp:97-125 transcribed as loops (chunking, remainder on chunk T-1, / max length)."""
     L = min(len(s1), len(s2))
@@ -237,7 +301,77 @@ def test_wait_loops_are_wave_uniform():
     res = W.scan(so)
     with_loops = {k: v for k, v in res.items() if v["loops"]}
     for prefix in ("_ZN3msa11flow_kernel", "_ZN3msa11band_kernel", "_ZN3msa13stripe_kernel",
+                   "_ZN3msa12cflow_kernel",
                    "_ZN3msa10fill_block", "_ZN3msa14fill_block_aff", "_ZN3msa14fill_block_got"):
         assert any(k.startswith(prefix) for k in with_loops), f"no wait loop found in {prefix}*"
     bad = {k: v["bad"] for k, v in with_loops.items() if v["bad"]}
     assert not bad, f"exec-mask controlled wait loops: {bad}"
+
+
+def _isa_hazards():
+    import importlib.util
+
+    sys.path.insert(0, str(ROOT / "scripts"))
+    spec = importlib.util.spec_from_file_location("isa_hazards", ROOT / "scripts" / "isa_hazards.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_asm_hazard_detector():
+    """The detector on hand-written code.  DPP: one instruction after the VALU write of its source is short
+    (1 wait state of the 2 gfx950 needs); an `s_nop 1`, or two instructions, in between make it clean; a
+    write reaching the DPP through a branch to its block counts; so does a write of the DPP's destination
+    (the `old` value of lanes with no source lane); SGPR / VCC writes do not.  The other classes: M0 ->
+    LDS add-TID (1), VALU SGPR write -> VMEM address (5), -> v_readlane lane select (4), v_cmpx -> DPP (5)."""
+    H = _isa_hazards()
+    dpp = (0x10c, "v_mov_b32_dpp", "v5, v1 wave_shr:1 row_mask:0xf bank_mask:0xf ")
+
+    def fn(*mid):
+        return [(0x100, "v_pk_max_i16", "v1, v1, v24 ")] + [(0x104 + 4 * k, mn, o) for k, (mn, o) in
+                                                               enumerate(mid)] + [dpp, (0x200, "s_endpgm", " ")]
+
+    bad = H.hazards(fn(("v_pk_add_u16", "v2, v3, v4 ")))
+    assert [(b[0], b[5], b[6]) for b in bad] == [("dpp_vgpr", 1, [1])]
+    assert H.hazards(fn(("v_pk_add_u16", "v2, v3, v4 "), ("s_nop", "0 "))) == []
+    assert H.hazards(fn(("s_nop", "1 "))) == []
+    assert len(H.hazards(fn(("s_nop", "0 ")))) == 1
+    assert H.hazards(fn(("v_cmp_gt_i32_e32", "vcc, v1, v2 "), ("v_readfirstlane_b32", "s4, v1 "))) == []
+    # destination written one instruction before the DPP
+    assert len(H.hazards([(0x100, "v_add_u32_e32", "v5, 1, v5 "), (0x104, "s_nop", "0 "), (0x108,) + dpp[1:]])) == 1
+    # a branch from a block ending in the write, over clean fall-through code
+    br = [(0x100, "v_mov_b32_e32", "v1, 0 "), (0x104, "s_cbranch_scc1", "4 <f+0x18>"),
+          (0x108, "s_nop", "4 "), (0x10c, "s_nop", "4 "), (0x110, "s_branch", "3 <f+0x20>"),
+          (0x114, "s_nop", "0 "), (0x118,) + dpp[1:], (0x11c, "s_endpgm", " ")]
+    assert len(H.hazards(br)) == 1
+    # the other classes, short and padded
+    m0 = [(0x100, "s_mov_b32", "m0, s3 "), (0x104, "ds_write_addtid_b32", "v1 offset:0 ")]
+    assert [b[0] for b in H.hazards(m0)] == ["m0_lds"]
+    assert H.hazards([m0[0], (0x104, "s_nop", "0 "), (0x108,) + m0[1][1:]]) == []
+    vm = [(0x100, "v_readfirstlane_b32", "s4, v1 "), (0x104, "s_nop", "3 "), (0x108, "global_load_dword", "v2, v3, s[4:5] ")]
+    assert [b[0] for b in H.hazards(vm)] == ["sgpr_vmem"]
+    assert H.hazards([vm[0], (0x104, "s_nop", "4 "), vm[2]]) == []
+    ls = [(0x100, "v_readfirstlane_b32", "s4, v1 "), (0x104, "s_nop", "2 "), (0x108, "v_readlane_b32", "s6, v2, s4 ")]
+    assert [b[0] for b in H.hazards(ls)] == ["lane_select"]
+    assert H.hazards([ls[0], (0x104, "s_nop", "3 "), ls[2]]) == []
+    cx = [(0x100, "v_cmpx_gt_i32_e32", "vcc, v1, v2 "), (0x104, "s_nop", "3 "), (0x108,) + dpp[1:]]
+    assert [b[0] for b in H.hazards(cx)] == ["dpp_exec"]
+
+
+def test_asm_hazards_have_their_wait_states():
+    """Every kernel and device function in libmsa.so's gfx950 code object gives each software-managed
+    hazard its wait states on every control-flow path: VALU-write -> DPP-read (2), VALU EXEC write -> DPP
+    (5), M0 -> LDS add-TID / LDS-DMA (1), VALU SGPR write -> VMEM (5) and -> lane select (4).  hipcc pads
+    what it emits; inline asm is not padded -- round 5's cflow_kernel had 47 DPPs reading X one wait state
+    after the v_pk_max_i16 that wrote it, correct only by issue timing."""
+    H = _isa_hazards()
+    so = ROOT / "cse305_parallel_sequence_alignment_amd" / "libmsa.so"
+    if not so.exists():
+        pytest.skip("libmsa.so not built")
+    res = H.scan(so)
+    for prefix in ("_ZN3msa11flow_kernel", "_ZN3msa11band_kernel", "_ZN3msa13stripe_kernel",
+                   "_ZN3msa12cflow_kernel", "_ZN3msa14fill_block_aff", "_ZN3msa14fill_block_got"):
+        assert any(k.startswith(prefix) and v[0].get("dpp_vgpr") for k, v in res.items()), f"no DPP in {prefix}*"
+    assert any(v[0].get("m0_lds") for k, v in res.items() if "traceback_kernel" in k), "no LDS-DMA in the walk"
+    bad = {k: v[1][:3] for k, v in res.items() if v[1]}
+    assert not bad, f"hazards short of their wait states: {bad}"
