@@ -40,10 +40,15 @@ def build(quiet: bool = True) -> None:
         print(out.stdout)
 
 
+# MSA_ORACLE_DIR: load liboracle.so / librowsweep.so from another build of the same sources (the
+# sanitizer build, oracle/_san: tests/test_host.py::test_oracle_under_sanitizers)
+LIBDIR = Path(os.environ.get("MSA_ORACLE_DIR", str(HERE)))
+
+
 def lib():
     global _lib
     if _lib is None:
-        path = HERE / "liboracle.so"
+        path = LIBDIR / "liboracle.so"
         if not path.exists():
             build()
         L = C.CDLL(str(path))
@@ -258,7 +263,7 @@ def rowsweep(A: bytes, B: bytes, p: int = 1, mode: int = 1, g=1.0, h=2.0, match=
     Fills rows 1..rows (0 = all); returns (score, seconds)."""
     global _rowsweep
     if _rowsweep is None:
-        path = HERE / "librowsweep.so"
+        path = LIBDIR / "librowsweep.so"
         if not path.exists():
             build()
         L = C.CDLL(str(path))

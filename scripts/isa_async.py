@@ -165,20 +165,28 @@ def analyse(insts):
     return sorted(bad.values())
 
 
-def scan(so: Path, prefixes=None):
-    out = {}
-    for name, insts in waitloops.functions(waitloops.disassemble(so)).items():
-        if prefixes and not name.startswith(prefixes):
-            continue
-        out[name] = analyse(insts)
-    return out
+def _analyse_item(item):
+    return item[0], analyse(item[1])
+
+
+def scan(so: Path, prefixes=None, workers=1):
+    """{function: [early uses]}; workers > 1 analyses functions in that many processes."""
+    items = [(name, insts) for name, insts in waitloops.functions(waitloops.disassemble(so)).items()
+             if not prefixes or name.startswith(prefixes)]
+    if workers <= 1:
+        return dict(map(_analyse_item, items))
+    from concurrent.futures import ProcessPoolExecutor
+
+    items.sort(key=lambda it: -len(it[1]))  # largest first: the long kernels set the wall time
+    with ProcessPoolExecutor(workers) as ex:
+        return dict(ex.map(_analyse_item, items, chunksize=1))
 
 
 if __name__ == "__main__":
     so = Path(sys.argv[1]) if len(sys.argv) > 1 else Path(__file__).resolve().parent.parent / \
         "cse305_parallel_sequence_alignment_amd" / "libmsa.so"
     total = 0
-    for name, bad in sorted(scan(so).items()):
+    for name, bad in sorted(scan(so, workers=8).items()):
         total += len(bad)
         if bad:
             print(f"{len(bad):4d} early uses  {name[:110]}")

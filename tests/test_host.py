@@ -1,5 +1,6 @@
 """Host-side logic on CPU: the C-ABI library, stripe geometry, SW oracle vs brute force."""
 import ctypes as C
+import os
 import re
 import sys
 
@@ -375,3 +376,52 @@ def test_asm_hazards_have_their_wait_states():
     assert any(v[0].get("m0_lds") for k, v in res.items() if "traceback_kernel" in k), "no LDS-DMA in the walk"
     bad = {k: v[1][:3] for k, v in res.items() if v[1]}
     assert not bad, f"hazards short of their wait states: {bad}"
+
+
+def test_async_loads_are_waited_for():
+    """No instruction of libmsa.so's gfx950 code object reads or overwrites the destination of an LDS or
+    global load before an s_waitcnt covers it (scripts/isa_async.py: dataflow over every function's
+    control flow, DS in order / SMEM out of order on lgkmcnt, VMEM in order on vmcnt).  The flow, band and
+    cflow kernels issue their ring / counter reads as inline asm with explicit waits, which the compiler
+    does not count: a register copy or spill it placed between such a read and its wait would read a
+    value that has not landed."""
+    sys.path.insert(0, str(ROOT / "scripts"))
+    import isa_async as A  # (an importable module: the scan's worker processes unpickle its functions)
+
+    ins = [(0x100, "ds_read_b128", "v[4:7], v1 offset:16 "), (0x104, "v_mov_b32_e32", "v8, v5 "),
+           (0x108, "s_waitcnt", "lgkmcnt(0) "), (0x10c, "v_mov_b32_e32", "v9, v5 ")]
+    assert [b[0] for b in A.analyse(ins)] == [0x104]  # the detector itself
+    ins = [(0x100, "s_load_dwordx2", "s[4:5], s[0:1], 0x0 "), (0x104, "ds_read_b32", "v10, v1 "),
+           (0x108, "s_waitcnt", "lgkmcnt(1) "), (0x10c, "v_mov_b32_e32", "v9, v10 ")]
+    assert [b[0] for b in A.analyse(ins)] == [0x10c]  # SMEM may complete first: the DS read may not have
+    so = ROOT / "cse305_parallel_sequence_alignment_amd" / "libmsa.so"
+    if not so.exists():
+        pytest.skip("libmsa.so not built")
+    res = A.scan(so, prefixes=("_ZN3msa",), workers=min(8, os.cpu_count() or 1))
+    assert any(k.startswith("_ZN3msa12cflow_kernel") for k in res)
+    bad = {k: v[:3] for k, v in res.items() if v}
+    assert not bad, f"async results used before their wait: {bad}"
+
+
+def test_oracle_under_sanitizers():
+    """The CPU oracle (oracle/msa_oracle.c, oracle/cpu_rowsweep.cpp) built with AddressSanitizer and
+    UndefinedBehaviorSanitizer (every UB report aborts: partial.cpp's wrap semantics must be restated
+    without signed overflow), then tests/test_oracle_golden.py against it in a child process with the
+    sanitizer runtimes preloaded -- all the reference-produced fixtures, the KATs and the live comparison
+    with the reference's own code.  The multi-second at-size cases are left to the plain build."""
+    import subprocess
+
+    r = subprocess.run(["make", "-s", "-C", str(ROOT / "oracle"), "sanitize"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    gcc = lambda lib: subprocess.run(["gcc", f"-print-file-name={lib}"], capture_output=True,  # noqa: E731
+                                     text=True).stdout.strip()
+    env = dict(os.environ, LD_PRELOAD=f"{gcc('libasan.so')}:{gcc('libubsan.so')}",
+               ASAN_OPTIONS="detect_leaks=0:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1",
+               MSA_ORACLE_DIR=str(ROOT / "oracle" / "_san"))
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider",
+                        str(ROOT / "tests" / "test_oracle_golden.py"), "-k",
+                        "not at_size and not rowsweep_baseline_matches_oracle[8] and "
+                        "not rowsweep_baseline_matches_oracle[3]"],
+                       capture_output=True, text=True, env=env, cwd=str(ROOT), timeout=600)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    assert " passed" in r.stdout and "AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr
