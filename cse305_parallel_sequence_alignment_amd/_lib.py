@@ -76,6 +76,7 @@ def lib() -> C.CDLL:
     L.msa_device_count.argtypes = [C.POINTER(C.c_int)]
     L.msa_set_device_budget.argtypes = [C.c_int64]
     L.msa_device_budget_info.argtypes = [C.POINTER(C.c_int64)]
+    L.msa_device_memory_info.argtypes = [C.POINTER(C.c_int64)]
     L.msa_main_alignment.argtypes = [P, P, sz, sz, sz, C.c_double, C.c_double, P, sz, C.POINTER(sz),
                                      C.POINTER(C.c_double)]
     L.msa_subproblem.argtypes = [P, P, sz, sz, sz, sz, C.c_int, C.c_int, C.c_double, C.c_double, P, P, P, P, sz,
@@ -133,7 +134,7 @@ class _Bind:
 
 # Every symbol include/msa.h declares (checked by the CPU test suite).
 EXPORTED = [
-    "msa_status_string", "msa_version", "msa_device_count", "msa_set_device_budget", "msa_device_budget_info", "msa_main_alignment", "msa_subproblem",
+    "msa_status_string", "msa_version", "msa_device_count", "msa_set_device_budget", "msa_device_budget_info", "msa_device_memory_info", "msa_main_alignment", "msa_subproblem",
     "msa_non_parallel_tables", "msa_optimal_alignment", "msa_main_alignment_partitioned",
     "msa_subproblem_f64", "msa_subproblem_row",
     "msa_partial_partition", "msa_partial_tables", "msa_partition_tables", "msa_plan_create", "msa_plan_destroy", "msa_plan_cells_size",

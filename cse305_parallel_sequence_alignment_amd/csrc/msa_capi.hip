@@ -163,6 +163,13 @@ class DevPool {
     std::lock_guard<std::mutex> lk(mu_);
     return cached_;
   }
+  size_t cached(int dev) {  // free blocks of device dev
+    std::lock_guard<std::mutex> lk(mu_);
+    size_t b = 0;
+    for (const auto& e : free_)
+      if (e.first.first == dev) b += e.first.second;
+    return b;
+  }
 
  private:
   static constexpr size_t kCap = size_t(8) << 30;  // bytes kept cached (HBM is 288 GB)
@@ -186,6 +193,14 @@ DevPool& dev_pool() {
 // waits -- FIFO, so no caller is overtaken -- until it fits.  A call larger than the whole budget
 // runs alone (it waits until nothing else is admitted).  Budget: MSA_DEVICE_BUDGET_MB, else 90% of
 // the device's memory; msa_set_device_budget overrides it at run time.
+// Memory the library holds on a device outside the admitted calls: idle cached plans of the reference
+// walk and free blocks of the device pool (msa_refapi.inc).  An admission that would put admitted +
+// idle bytes over the budget first releases the idle ones, so cached memory never pushes admitted calls
+// into the allocator's out-of-memory path.
+size_t idle_device_bytes(int dev);
+size_t idle_plan_bytes(int dev);
+void reclaim_idle_device_bytes(int dev);
+
 class Admission {
  public:
   void acquire(int dev, size_t bytes) {
@@ -203,7 +218,14 @@ class Admission {
     d.admitted++;
     if (waited) d.waits++;
     d.serving++;
+    const size_t inuse = d.inuse, budget = d.budget;
     cv_.notify_all();  // the next ticket may fit too
+    lk.unlock();
+    if (inuse + idle_device_bytes(dev) > budget) {
+      reclaim_idle_device_bytes(dev);
+      std::lock_guard<std::mutex> lk2(mu_);
+      get(dev).reclaims++;
+    }
   }
   void release(int dev, size_t bytes) {
     std::lock_guard<std::mutex> lk(mu_);
@@ -216,10 +238,10 @@ class Admission {
     Dev& d = get(dev);
     d.budget = bytes ? bytes : default_budget(dev);
     d.peak = d.inuse;
-    d.waits = d.admitted = 0;
+    d.waits = d.admitted = d.reclaims = 0;
     cv_.notify_all();
   }
-  void info(int dev, int64_t* out) {
+  void info(int dev, int64_t* out, int n = 5) {
     std::lock_guard<std::mutex> lk(mu_);
     Dev& d = get(dev);
     out[0] = (int64_t)d.budget;
@@ -227,13 +249,14 @@ class Admission {
     out[2] = (int64_t)d.peak;
     out[3] = (int64_t)d.waits;
     out[4] = (int64_t)d.admitted;
+    if (n > 5) out[5] = (int64_t)d.reclaims;
   }
 
  private:
   struct Dev {
     bool init = false;
     size_t budget = 0, inuse = 0, peak = 0;
-    uint64_t next = 0, serving = 0, waits = 0, admitted = 0;
+    uint64_t next = 0, serving = 0, waits = 0, admitted = 0, reclaims = 0;
   };
   static size_t default_budget(int dev) {
     const char* e = std::getenv("MSA_DEVICE_BUDGET_MB");
@@ -490,6 +513,7 @@ struct msa_plan {
   bool band_k = false;  // band_kernel (banded single pair, msa_band.hip)
   int band_items = 0;   // band_kernel: items of the larger of its launches (granule slots)
   bool flow2 = false;  // + pass-2 blocks inside the same launch (O_H)
+  bool fused_reduce = false;  // the pass-2 blocks write the pair result (fl_block_done): no reduce launch
   bool cflow = false;  // cflow_kernel: packed-couple score-only batch as flag-synchronised chains
   kfn_t fill_fn = nullptr;  // long pairs: pass 2 as a launch of its own behind pass 1
   int fill_grid = 0;
@@ -503,6 +527,7 @@ struct msa_plan {
   int R = 1;      // flow kernel rows per lane
   int nflow = 0;  // two-pass: pass-1 workgroups (the rest of the grid runs pass-2 blocks)
   int brw = 0, nseg = 0, nblk = 0;
+  int ps = FL_PS;  // phases per pass-2 segment (FL_PS_FILL when pass 2 is a launch of its own)
   int gbuf_stride = 0;
   kfn_t fn = nullptr;
   // device
@@ -591,6 +616,20 @@ int msa_device_budget_info(int64_t* out5) {
   int rc = ensure_device();
   if (rc != MSA_OK) return rc;
   admission().info(current_device(), out5);
+  return MSA_OK;
+}
+
+int msa_device_memory_info(int64_t* out4) {
+  if (!out4) return MSA_ERR_ARG;
+  int rc = ensure_device();
+  if (rc != MSA_OK) return rc;
+  const int dev = current_device();
+  int64_t b[6];
+  admission().info(dev, b, 6);
+  out4[0] = b[1];
+  out4[1] = (int64_t)idle_plan_bytes(dev);
+  out4[2] = (int64_t)dev_pool().cached(dev);
+  out4[3] = b[5];
   return MSA_OK;
 }
 
@@ -712,6 +751,13 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
                     desc->m[0] > 0 && flow_lds <= device_lds_max();
   P->flow = flow;
   P->flow2 = flow && (out_mode == MSA_OUT_H || aff);
+  {
+    // SW two-pass plans reduce their pair result inside the launch when the cell index fits 32 bits
+    // (MSA_FUSED_REDUCE=0: the reduce_blocks_kernel launch, for A/B)
+    const char* fr = std::getenv("MSA_FUSED_REDUCE");
+    const int64_t cells1 = (desc->m[0] + 1) * (desc->n[0] + 1);
+    P->fused_reduce = P->flow2 && kalg != MSA_ALG_REF1 && cells1 < (int64_t(1) << 32) && !(fr && fr[0] == '0');
+  }
   const int W = flow ? FL_W : (single ? MSA_WAVES_SINGLE : MSA_WAVES_BATCH);
   P->W = W;
   const int KS = flow ? 16 : (single ? ks_single(kalg) : ks_batch(kalg));
@@ -902,7 +948,7 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
     kp.lds_code_bytes = fl_code_bytes((int)desc->n[0]);
     P->lds_bytes = flow_lds;
     // pass-2 blocks: FL_P2INTS ints per wave (inputs + column codes staged in LDS)
-    if (P->flow2) P->lds_bytes = std::max(flow_lds, (size_t)(FL_W + 2) * FL_P2INTS * 4);
+    if (P->flow2) P->lds_bytes = std::max(flow_lds, (size_t)(FL_W + 2) * fl_p2ints(FL_PS) * 4);
   }
   if (P->lds_bytes > device_lds_max()) {
     std::fprintf(stderr, "msa: problem needs %zu B of LDS per workgroup (> %zu B, the device's limit)\n",
@@ -950,7 +996,8 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
         P->grid = P->nflow;
         P->fill_fn = pick_fill(kalg, tp, P->R, desc->match >= 0 && desc->mismatch >= 0);
         if (!P->fill_fn) { delete P; return MSA_ERR_UNSUPPORTED; }
-        P->fill_lds = (size_t)FL_FILLW * FL_P2INTS * 4;
+        P->fill_lds = (size_t)FL_FILLW * fl_p2ints(FL_PS_FILL) * 4;
+        P->ps = FL_PS_FILL;  // its blocks are segments of FL_PS_FILL phases (pass 1 saves state that often)
         const int focc = kernel_shape(P->fill_fn, FL_FILLW * 64, P->fill_lds);
         if (focc < 0) { delete P; return MSA_ERR_HIP; }
         P->fill_grid = ncu * std::max(1, std::min(focc, 8));
@@ -1144,15 +1191,15 @@ int msa_plan_create(const msa_plan_desc* desc, msa_plan** out) {
   if (P->flow2) {
     const int S = (int)((desc->m[0] + 64 * P->R - 1) / (64 * P->R));
     P->brw = 16 * P->pairs[0].pmax + 16;
-    P->nseg = (P->pairs[0].pmax + FL_PS - 1) / FL_PS;
+    P->nseg = (P->pairs[0].pmax + P->ps - 1) / P->ps;
     P->nblk = S * P->nseg;
     // pass-2 blocks in expected readiness order: stripe s starts ~6.5 phases after
-    // stripe s-1, and segment seg is complete FL_PS (seg + 1) phases after its start
+    // stripe s-1, and segment seg is complete ps (seg + 1) phases after its start
     std::vector<int> order(P->nblk);
     std::vector<double> key(P->nblk);
     for (int b = 0; b < P->nblk; ++b) {
       order[b] = b;
-      key[b] = (P->R == 2 ? 7.5 : 6.5) * (b / P->nseg) + (double)FL_PS * (b % P->nseg + 1);
+      key[b] = (P->R == 2 ? 7.5 : 6.5) * (b / P->nseg) + (double)P->ps * (b % P->nseg + 1);
     }
     std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return key[x] < key[y]; });
     // (affine: the F~ bottom rows follow the Z rows; a snapshot is 4 values per lane)
@@ -1253,8 +1300,10 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
   a.blk = P->d_blk;
   a.border = P->d_order;
   a.nflow = P->nflow;
+  a.best_key = P->fused_reduce ? reinterpret_cast<unsigned long long*>(P->d_ticket + MSA_TK_BEST) : nullptr;
   a.brw = P->brw;
   a.nseg = P->nseg;
+  a.ps_shift = __builtin_ctz((unsigned)P->ps);
   a.nblk = P->nblk;
   {
     const unsigned virt = (P->kp.alg == MSA_ALG_SWL || P->kp.alg == MSA_ALG_SWL0 || P->kp.alg == MSA_ALG_SWLP ||
@@ -1310,8 +1359,10 @@ int msa_plan_run(msa_plan* P, const uint8_t* dA, const uint8_t* dB, void* c0, vo
   }
   if (ev) HIPCHK(hipEventRecord(P->ev1, st));
   if (P->flow2 && P->kp.alg != MSA_ALG_REF1) {  // (Gotoh: the final state is in the last stripe's meta)
-    hipLaunchKernelGGL(reduce_blocks_kernel, dim3(1), dim3(1024), 0, st, (const int4*)P->d_blk, P->nblk, P->d_res);
-    HIPCHK(hipGetLastError());
+    if (!P->fused_reduce) {  // (fused: the pass-2 blocks folded the result into the best-cell key)
+      hipLaunchKernelGGL(reduce_blocks_kernel, dim3(1), dim3(1024), 0, st, (const int4*)P->d_blk, P->nblk, P->d_res);
+      HIPCHK(hipGetLastError());
+    }
     return MSA_OK;
   }
   const int sw = (P->kp.alg == MSA_ALG_SWL || P->kp.alg == MSA_ALG_SWL0 || P->kp.alg == MSA_ALG_SWLP ||
@@ -1346,9 +1397,17 @@ int msa_plan_results(msa_plan* P, msa_pair_result* out, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   int err = 0;
   HIPCHK(hipMemcpyAsync(&err, P->d_err, sizeof(err), hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(out, P->d_res, sizeof(PairResult) * P->d.n_pairs, hipMemcpyDeviceToHost, st));
+  unsigned long long key = 0;
+  if (P->fused_reduce)  // one pair: its result is the pass-2 blocks' best-cell key
+    HIPCHK(hipMemcpyAsync(&key, P->d_ticket + MSA_TK_BEST, sizeof(key), hipMemcpyDeviceToHost, st));
+  else
+    HIPCHK(hipMemcpyAsync(out, P->d_res, sizeof(PairResult) * P->d.n_pairs, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   static_assert(sizeof(PairResult) == sizeof(msa_pair_result), "result layout");
+  if (P->fused_reduce) {
+    const PairResult r = best_key_decode(key, P->pairs[0].n);
+    std::memcpy(out, &r, sizeof(r));
+  }
   if (err) {
     std::fprintf(stderr, "msa: a kernel wait hit its spin limit (site %d) in a run since the plan was created "
                  "or last cleared\n", err);
@@ -1406,6 +1465,12 @@ int msa_plan_scores(msa_plan* P, int32_t* dst, void* stream) {
   if (!P || !dst) return MSA_ERR_ARG;
   // the score field of every PairResult, device to device (no host sync)
   P->note_stream((hipStream_t)stream);
+  if (P->fused_reduce) {  // the pair result from the best-cell key first
+    hipLaunchKernelGGL(best_key_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                       reinterpret_cast<const unsigned long long*>(P->d_ticket + MSA_TK_BEST), (long long)P->pairs[0].n,
+                       P->d_res);
+    HIPCHK(hipGetLastError());
+  }
   HIPCHK(hipMemcpy2DAsync(dst, sizeof(int32_t), P->d_res, sizeof(PairResult), sizeof(int32_t), (size_t)P->d.n_pairs,
                           hipMemcpyDeviceToDevice, (hipStream_t)stream));
   return MSA_OK;
@@ -1429,7 +1494,8 @@ int msa_plan_traceback(msa_plan* P, int64_t pair, const uint8_t* dDir, uint8_t* 
   P->note_stream(st);
   hipLaunchKernelGGL((P->R == 2 ? traceback_kernel<TB_SW, 2> : traceback_kernel<TB_SW>), dim3(1), dim3(64), 0, st, dDir, P->d_pairs, P->d_meta,
                      (const PairResult*)P->d_res, (int)pair, 0, 0, d_ops, (long long)ops_cap, (long long*)d_info,
-                     P->flow ? 1 : 0);
+                     P->flow ? 1 : 0,
+                     P->fused_reduce ? reinterpret_cast<const unsigned long long*>(P->d_ticket + MSA_TK_BEST) : nullptr);
   HIPCHK(hipGetLastError());
   return MSA_OK;
 }
@@ -1446,7 +1512,8 @@ int msa_plan_traceback_gotoh(msa_plan* P, int64_t pair, int end_type, const uint
   hipLaunchKernelGGL(P->kp.alg == MSA_ALG_REF1 ? (P->R == 2 ? traceback_kernel<TB_REF_TAG, 2> : traceback_kernel<TB_REF_TAG>)
                                                : traceback_kernel<TB_REF>, dim3(1),
                      dim3(64), 0, st, dDir, P->d_pairs, P->d_meta, (const PairResult*)P->d_res, (int)pair, end_type,
-                     (int)P->kp.h, d_ops, (long long)ops_cap, (long long*)d_info, P->flow ? 1 : 0);
+                     (int)P->kp.h, d_ops, (long long)ops_cap, (long long*)d_info, P->flow ? 1 : 0,
+                     (const unsigned long long*)nullptr);
   HIPCHK(hipGetLastError());
   return MSA_OK;
 }

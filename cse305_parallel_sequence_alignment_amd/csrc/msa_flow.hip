@@ -25,10 +25,10 @@
 //     the workgroup (the previous workgroup's {epoch, value} granules, or row 0);
 //   * io-out: every link's blocks -> the bottom-row array BR (pass 2's input),
 //     the last link's also -> {epoch, value} granules for the next workgroup;
-//   * every FL_PS phases each lane's state (left, diagonal) -> SNAP;
+//   * every segment (FL_PS phases, FL_PS_FILL for a separate pass-2 launch) each lane's state -> SNAP;
 //   * items (W stripes) come from 8 per-XCD ticket chunks: consecutive items
 //     share an L2, and an item only ever waits on an earlier one.
-// Pass 2 (fill_kernel): every (stripe, FL_PS-phase segment) block restarts
+// Pass 2 (fill_kernel): every (stripe, segment) block restarts
 // from SNAP and BR, recomputes its cells with the same instructions, writes
 // int32 H in the skewed stripe layout (coalesced non-temporal 1 KiB stores)
 // and reduces its best cell.  Thousands of independent blocks fill the chip,
@@ -58,20 +58,27 @@ namespace msa {
 // linear (stride L8 + 16, no wrap) and io-in never holds blocks back for ring space: the ring's
 // refill bookkeeping measured +6 us on C2 (10k, 0.459 -> 0.465 ms).
 #ifndef FL_PS
-#define FL_PS 8         // phases per pass-2 segment (pass 1 saves its state every FL_PS phases)
-#endif
-// A pass-2 wave's LDS area (p2_stage): two value streams of FL_P2VS ints (the row above the block's
-// 16 FL_PS columns), then the column codes its phases read, one staged dword per lane and round.
-// Lane r of phase k reads code dwords (63 - r + 16 k) / 4 + [0, 5), i.e. up to (63 + 16 (FL_PS - 1)) / 4
-// + 4: 48 dwords at FL_PS = 8, 80 at 16.  Round 5 staged a fixed 64 dwords, so a -DFL_PS=16 build read
+#define FL_PS 8         // phases per pass-2 segment of the in-launch pass 2 (pass 1 saves its state every
+#endif                  // segment: KArgs::ps_shift, the plan's segment length)
+#ifndef FL_PS_FILL
+#define FL_PS_FILL 32   // ... of the separate pass-2 launch (flow_fill_kernel, long pairs): fewer, longer
+#endif                  // blocks stage SNAP + BR less often (97k ref: 15.70 -> 13.02 ms at 32, 13.36 at 16)
+// A pass-2 wave's LDS area (p2_stage): two value streams of fl_p2vs(PS) ints (the row above the block's
+// 16 PS columns), then the column codes its phases read, one staged dword per lane and round.
+// Lane r of phase k reads code dwords (63 - r + 16 k) / 4 + [0, 5), i.e. up to (63 + 16 (PS - 1)) / 4
+// + 4: 48 dwords at PS = 8, 144 at 32.  Round 5 staged a fixed 64 dwords, so a 16-phase build read
 // its last phases' codes from the next wave's area (a wrong direction-byte plane, a wrong 97k walk
-// with the right score); the span now follows FL_PS.
-#define FL_P2VS (16 * FL_PS > 256 ? 16 * FL_PS : 256)  // ints per value stream
-#define FL_P2CODW ((63 + 16 * (FL_PS - 1)) / 4 + 5)     // code dwords a block's phases read
-#define FL_P2COD ((FL_P2CODW + 63) / 64 * 64)           // staged: whole rounds of 64 lanes
-#define FL_P2INTS (2 * FL_P2VS + FL_P2COD)              // 576 at FL_PS = 8 and 16
-static_assert(16 * FL_PS <= FL_P2VS, "a value stream holds the row above FL_PS phases of 16 columns");
-static_assert(FL_P2CODW <= FL_P2COD, "the staged code span covers every code dword the phases read");
+// with the right score); the span now follows the segment length.
+constexpr int fl_ps(int caller) { return caller ? FL_PS_FILL : FL_PS; }
+constexpr int fl_p2vs(int ps) { return 16 * ps > 256 ? 16 * ps : 256; }     // ints per value stream
+constexpr int fl_p2codw(int ps) { return (63 + 16 * (ps - 1)) / 4 + 5; }  // code dwords a block's phases read
+constexpr int fl_p2cod(int ps) { return (fl_p2codw(ps) + 63) / 64 * 64; } // staged: whole rounds of 64 lanes
+constexpr int fl_p2ints(int ps) { return 2 * fl_p2vs(ps) + fl_p2cod(ps); } // 576 at PS = 8, 1216 at 32
+static_assert(fl_p2ints(FL_PS) == 576 || FL_PS != 8, "in-launch pass-2 LDS area");
+static_assert(16 * FL_PS <= fl_p2vs(FL_PS) && 16 * FL_PS_FILL <= fl_p2vs(FL_PS_FILL),
+              "a value stream holds the row above a segment's 16-column phases");
+static_assert(fl_p2codw(FL_PS_FILL) <= fl_p2cod(FL_PS_FILL), "the staged code span covers every code dword read");
+static_assert((FL_PS & (FL_PS - 1)) == 0 && (FL_PS_FILL & (FL_PS_FILL - 1)) == 0, "segments: powers of two");
 #define FL_FILLW 4      // waves per workgroup of the separate pass-2 launch (flow_fill_kernel)
 #define FL_SPIN_MAX (1u << 26)  // a spin limit sets err = the site's code (10..15) instead of hanging
 #ifndef FL_PF
@@ -357,6 +364,7 @@ struct FillArgs {
   int oe;           // affine: gap_open - gap_extend (g = gap_extend); Gotoh: h
   msa_stripe_meta* meta;  // Gotoh: the final cell's tables go to the last stripe's meta
   int stripe0;
+  unsigned long long* best_key;  // SW: the pair's best-cell key (fl_block_result), or nullptr
 #ifdef MSA_STAMPS
   unsigned long long* stamps;  // diagnostic: pass-2 block tick totals (FL_P2STAT)
 #endif
@@ -373,6 +381,23 @@ struct FillArgs {
 // FillArgs built in SGPRs) and get their wave's LDS area as an LDS pointer: no by-value struct on the
 // stack, so the kernel needs no scratch (a stack copy of FillArgs per call cost the launch its scratch
 // setup and every access a private-memory load).
+// The pair result of a two-pass SW plan, folded by the pass-2 blocks themselves when best_key is set
+// (msa_plan_create: (m + 1)(n + 1) < 2^32): lane 0 of a block folds the block's best into one 64-bit key
+// with a non-returning atomicMax -- score, then the first cell in row-major order, reduce_blocks_kernel's
+// rule -- instead of storing it for a reduce_blocks_kernel launch (that launch, ~5 us, and its dispatch
+// gap, ~6 us, leave C2's step).  Readers decode the key (best_key_decode).  Measured and not kept: the
+// last block writing the PairResult itself -- a done counter and two __threadfence, which made every
+// pass-2 wave wait for its cell stores: C2 kernel 0.466 -> 0.477 ms.
+__device__ __forceinline__ void fl_block_result(int4* blk_out, unsigned long long* best_key, int blk, int lane, int bb,
+                                                int bi, int bj, int n) {
+  if (lane != 0) return;
+  if (best_key) {
+    const unsigned lo = bb > 0 ? ~(unsigned)((unsigned long long)bi * (unsigned)(n + 1) + (unsigned)bj) : 0xffffffffu;
+    atomicMax(best_key, ((unsigned long long)((unsigned)bb ^ 0x80000000u) << 32) | lo);
+  } else {
+    blk_out[blk] = make_int4(bb, bi, bj, 0);
+  }
+}
 typedef const __attribute__((address_space(4))) struct KArgs kargs_c;
 __device__ __forceinline__ FillArgs fill_args_of(kargs_c* k) {
   // (measured: the pointer made wave-uniform -- scalar loads of the arguments instead of vector loads --
@@ -380,7 +405,7 @@ __device__ __forceinline__ FillArgs fill_args_of(kargs_c* k) {
   const msa_pair_desc pd = k->pairs[0];
   return FillArgs{k->A, k->cod, k->br, k->snap, k->outH, k->blk, k->err, k->cod_copy, pd.a_off, pd.cod_off,
                   pd.out_off, pd.m, pd.n, pd.pmax, k->nseg, k->brw, k->kp.match, k->kp.mismatch, k->kp.gap_ext,
-                  k->kp.epoch, k->outDir, k->kp.gap_open - k->kp.gap_ext, k->meta, pd.stripe0
+                  k->kp.epoch, k->outDir, k->kp.gap_open - k->kp.gap_ext, k->meta, pd.stripe0, k->best_key
 #ifdef MSA_STAMPS
                   , k->stamps
 #endif
@@ -474,7 +499,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
         t = __builtin_amdgcn_readlane(t, 0);
         if (t >= a.nblk) break;
         kargs_c* ka = (kargs_c*)__builtin_amdgcn_kernarg_segment_ptr();  // (a is the only argument)
-        lds_int* wl = L(smem + w * FL_P2INTS);
+        lds_int* wl = L(smem + w * fl_p2ints(FL_PS));
         if constexpr (GOT && R == 2) fill_block_got2<0>(ka, a.border[t], lane, wl);
         else if constexpr (GOT) fill_block_got<0>(ka, a.border[t], lane, wl);
         else if constexpr (AFF && R == 2) fill_block_aff2<0>(ka, a.border[t], lane, wl);
@@ -861,11 +886,11 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
           ds_reread_b128x4(ra + 1024u, F);
           if constexpr (MASK) mask_in(q, Z, F);
         }
-        if (q % FL_PS == 0) {  // pass 2 restarts here: each lane's (Z left, E~, F~, diagonal Z)
+        if ((q & ((1 << a.ps_shift) - 1)) == 0) {  // pass 2 restarts here: each lane's (Z left, E~, F~, diagonal Z)
           if constexpr (R == 2) {  // rows 1 and 2: H~, R~, diagonal H~ / H~, R~, D~ (pass 2: unshifted)
             // (affine: Z left, E~, diagonal Z / Z left, E~, F~)
             constexpr int SH = GOT ? 1 : 0;
-            unsigned long long* sp = a.snap + ((size_t)k * a.nseg + q / FL_PS) * 384 + lane;
+            unsigned long long* sp = a.snap + ((size_t)k * a.nseg + (q >> a.ps_shift)) * 384 + lane;
             gstore(sp, ((unsigned long long)ep << 32) | (unsigned)Zl);
             gstore(sp + 64, ((unsigned long long)ep << 32) | (unsigned)(E - SH * 4 * oe));
             gstore(sp + 128, ((unsigned long long)ep << 32) | (unsigned)U);
@@ -873,7 +898,7 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
             gstore(sp + 256, ((unsigned long long)ep << 32) | (unsigned)(E2 - SH * 4 * oe));
             gstore(sp + 320, ((unsigned long long)ep << 32) | (unsigned)(Fo2 - SH * 4 * oe));
           } else {
-            unsigned long long* sp = a.snap + ((size_t)k * a.nseg + q / FL_PS) * 256 + lane;
+            unsigned long long* sp = a.snap + ((size_t)k * a.nseg + (q >> a.ps_shift)) * 256 + lane;
             gstore(sp, ((unsigned long long)ep << 32) | (unsigned)Zl);
             gstore(sp + 64, ((unsigned long long)ep << 32) | (unsigned)(GOT ? E - 4 * oe : E));  // pass 2: R~, D~
             gstore(sp + 128, ((unsigned long long)ep << 32) | (unsigned)(GOT ? Fo - 4 * oe : Fo));
@@ -1241,8 +1266,8 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
           if constexpr (MASK) mask_in(q, IN);
         }
         if constexpr (SAVE && (MSA_ABL & 2) == 0) {
-          if (q % FL_PS == 0) {  // pass 2 restarts here: each lane's left and diagonal values
-            unsigned long long* sp = a.snap + ((size_t)k * a.nseg + q / FL_PS) * (128 * R) + lane;
+          if ((q & ((1 << a.ps_shift) - 1)) == 0) {  // pass 2 restarts here: each lane's left and diagonal values
+            unsigned long long* sp = a.snap + ((size_t)k * a.nseg + (q >> a.ps_shift)) * (128 * R) + lane;
             gstore(sp, ((unsigned long long)ep << 32) | (unsigned)X);
             gstore(sp + 64, ((unsigned long long)ep << 32) | (unsigned)U);
             if constexpr (R == 2) gstore(sp + 128, ((unsigned long long)ep << 32) | (unsigned)X2);
@@ -1367,52 +1392,55 @@ __global__ __launch_bounds__((FL_W + 2) * 64) __attribute__((amdgpu_waves_per_eu
 #endif
 }
 
-// A pass-2 block's inputs are staged in its wave's LDS area (FL_P2INTS ints) before the phase loop:
-// the row above its FL_PS phases, value stream k at lds + FL_P2VS k (columns [0, nv) from the bottom-row
+// A pass-2 block's inputs are staged in its wave's LDS area (fl_p2ints(PS) ints) before the phase loop:
+// the row above its PS phases, value stream k at lds + fl_p2vs(PS) k (columns [0, nv) from the bottom-row
 // granules the caller loaded, row 0 for stripe 0, -inf past the producer's last block), and the column
-// codes the block reads -- columns cs - 63 + 16 q0 + [0, 4 FL_P2COD), one dword per lane and round from
-// an aligned staged copy -- at lds + 2 FL_P2VS.  The phase loop then issues no global load: a load in flight (codes
+// codes the block reads -- columns cs - 63 + 16 q0 + [0, 4 fl_p2cod(PS)), one dword per lane and round
+// from an aligned staged copy -- at lds + 2 fl_p2vs(PS).  The phase loop then issues no global load: a load in flight (codes
 // prefetched phases ahead) made every phase wait for the previous phases' H / direction stores too --
 // one vmcnt counter for both -- i.e. ~1 us per phase.  2.3 KiB per wave: pass-2 workgroups fit beside
 // a pass-1 one on a CU.
-template <int NV, class ROW0>
+template <int NV, int PS, class ROW0>
 __device__ __forceinline__ void p2_stage(lds_int* lds, int s, int nv, int ntot, int lane, ROW0 row0, const uint8_t* cod,
                                          long long cod_copy, int cs, int q0) {
+  constexpr int VS = fl_p2vs(PS), COD = fl_p2cod(PS);
   const int b = cs - 63 + 16 * q0 - 1 + MSA_CPAD;  // byte of that first column in copy 0 (>= 0: CPAD 256)
   const int c = b & (MSA_NCOPY - 1);              // copy c holds it at the 16-aligned byte b - c
-  unsigned w[FL_P2COD / 64];
+  unsigned w[COD / 64];
 #pragma unroll
-  for (int d = 0; d < FL_P2COD / 64; ++d) {
-    // (round 0 stays inside the copy: b + 256 <= the padded row; later rounds -- FL_PS > 12 -- are clamped
+  for (int d = 0; d < COD / 64; ++d) {
+    // (round 0 stays inside the copy: b + 256 <= the padded row; later rounds -- PS > 12 -- are clamped
     // to it, the dwords past the row's end are never read by a phase < P)
     const long long o = (b - c) + 4 * (64 * d + lane);
     w[d] = *reinterpret_cast<const unsigned*>(cod + (size_t)c * cod_copy + (d == 0 ? o : min(o, cod_copy - 4)));
   }
 #pragma unroll
   for (int k = 0; k < NV; ++k)
-    for (int v = (s == 0 ? 0 : nv) + lane; v < ntot; v += 64) *L(lds + FL_P2VS * k + v) = (s == 0) ? row0(v, k) : MSA_NEG;
+    for (int v = (s == 0 ? 0 : nv) + lane; v < ntot; v += 64) *L(lds + VS * k + v) = (s == 0) ? row0(v, k) : MSA_NEG;
 #pragma unroll
-  for (int d = 0; d < FL_P2COD / 64; ++d) *L(lds + 2 * FL_P2VS + 64 * d + lane) = (int)w[d];
+  for (int d = 0; d < COD / 64; ++d) *L(lds + 2 * VS + 64 * d + lane) = (int)w[d];
   FL_CBAR();  // (one wave's LDS ops execute in order: the phase loop's reads see these writes)
 }
 // Lane r's 16 column codes of the block's phase k (columns cs - r + 16 (q0 + k) + [0, 16)): five dwords
 // of the staged span and four byte-aligns (the shift (63 - r) mod 4 is the lane's for every phase).
+template <int PS>
 __device__ __forceinline__ fl_v4u p2_codes(lds_int* lds, int k, int lane) {
   const int o = (63 - lane) + 16 * k;
-  const lds_int* p = L(lds + 2 * FL_P2VS + (o >> 2));
+  const lds_int* p = L(lds + 2 * fl_p2vs(PS) + (o >> 2));
   const unsigned d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3], d4 = p[4];
   const unsigned sh = (unsigned)o & 3u;
   return fl_v4u{__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
                 __builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh)};
 }
 
-// Pass 2: block (stripe s, segment seg) of FL_PS phases, one wave.  Its inputs
+// Pass 2: block (stripe s, segment seg) of PS phases, one wave.  Its inputs
 // are {epoch, value} granules that pass 1 may still be writing: the wave waits
 // for the block's last bottom-row granule, then loads and checks them all.
 // R = 2: lane r holds rows 128s+2r+1 (X/U) and 128s+2r+2 (X2); cells go to the
 // R = 2 layout (per 4 steps: the wave's row-1 int4s, then its row-2 int4s).
 template <bool FLOOR, bool TRACKPOS, int R, int CALLER>
 __device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, int lane, lds_int* lds) {
+  constexpr int PS = fl_ps(CALLER);
   constexpr bool GS = !FLOOR;
   const unsigned ep = a.ep;
   const int m = a.m, n = a.n, S = (m + 64 * R - 1) / (64 * R), g = a.g;
@@ -1420,9 +1448,9 @@ __device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, 
   int bb = INT32_MIN, bi = 0, bj = 0;
   if (s < S) {
     const int P = fl_P(s, m, n, R);
-    const int q0 = seg * FL_PS;
+    const int q0 = seg * PS;
     if (q0 < P) {
-      int q1 = min(P, q0 + FL_PS);
+      int q1 = min(P, q0 + PS);
       const int cs = fl_cs(s);
       const int row_i = 64 * R * s + R * lane + 1;
       const unsigned ac = (row_i <= m) ? (a.A[a.a_off + row_i - 1] & 7u) : 0u;
@@ -1470,7 +1498,7 @@ __device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, 
         q1 = q0;  // nothing computed; the block reports no cell
       }
       // row 0 (stripe 0): H = 0 left of and on the top border
-      p2_stage<1>(lds, s, nv, 16 * (q1 - q0), lane,
+      p2_stage<1, PS>(lds, s, nv, 16 * (q1 - q0), lane,
                   [&](int v, int) { return GS ? g * (cs + 16 * q0 + v) : -g; }, a.cod + a.cod_off, a.cod_copy, cs, q0);
       // H = G - g(i+j); i+j = 64Rs + 1 + cs + t + (R-1) lane on row 1, +1 on row 2
       const int negct0 = -g * (64 * R * s + 1 + cs + (R - 1) * lane);
@@ -1492,7 +1520,7 @@ __device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, 
             IN[4 * u] = v.x; IN[4 * u + 1] = v.y; IN[4 * u + 2] = v.z; IN[4 * u + 3] = v.w;
           }
         }
-        const fl_v4u c4 = p2_codes(lds, q - q0, lane);
+        const fl_v4u c4 = p2_codes<PS>(lds, q - q0, lane);
         const unsigned cw[4] = {c4.x, c4.y, c4.z, c4.w};
         const int negct = negct0 - 16 * g * q;
         int hv[16], hv2[16];
@@ -1559,10 +1587,10 @@ __device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, 
     const int ob = __shfl_xor(bb, off), oi = __shfl_xor(bi, off), oj = __shfl_xor(bj, off);
     if (ob > bb || (ob == bb && (oi < bi || (oi == bi && oj < bj)))) { bb = ob; bi = oi; bj = oj; }
   }
-  if (lane == 0) a.blk[blk] = make_int4(bb, bi, bj, 0);
+  fl_block_result(a.blk, a.best_key, blk, lane, bb, bi, bj, a.n);
 }
 
-// Pass 2, affine (config C5): block (stripe s, segment seg) recomputes its FL_PS phases from
+// Pass 2, affine (config C5): block (stripe s, segment seg) recomputes its PS phases from
 // SNAP (Z left, E~, F~, diagonal Z per lane) and the stripe above's bottom row (Z and F~
 // granules), writes the direction bytes in the skewed stripe layout -- lane r's 16 bytes of a
 // phase are one 16-byte store, a wave's phase one contiguous 1 KiB -- and reduces its first
@@ -1570,6 +1598,7 @@ __device__ __attribute__((noinline)) void fill_block(const FillArgs a, int blk, 
 // traceback_kernel<TB_SW> reads them unchanged).
 template <int CALLER>
 __device__ __attribute__((noinline)) void fill_block_aff(kargs_c* ka, int blk, int lane, lds_int* lds) {
+  constexpr int PS = fl_ps(CALLER);
   const FillArgs a = fill_args_of(ka);
   const unsigned ep = a.ep;
   const int m = a.m, n = a.n, S = (m + 63) / 64, g = a.g, oe = a.oe;
@@ -1577,9 +1606,9 @@ __device__ __attribute__((noinline)) void fill_block_aff(kargs_c* ka, int blk, i
   int bb = INT32_MIN, bi = 0, bj = 0;
   if (s < S) {
     const int P = fl_P(s, m, n, 1);
-    const int q0 = seg * FL_PS;
+    const int q0 = seg * PS;
     if (q0 < P) {
-      int q1 = min(P, q0 + FL_PS);
+      int q1 = min(P, q0 + PS);
       const int cs = fl_cs(s);
       const int row_i = 64 * s + lane + 1;
       const unsigned ac = (row_i <= m) ? (a.A[a.a_off + row_i - 1] & 7u) : 0u;
@@ -1612,7 +1641,7 @@ __device__ __attribute__((noinline)) void fill_block_aff(kargs_c* ka, int blk, i
             const unsigned long long gz = gload(brz + 16 * q0 + v), gf = gload(brf + 16 * q0 + v);
             ok = ok && ((unsigned)(gz >> 32) == ep) && ((unsigned)(gf >> 32) == ep);
             *L(lds + v) = (int)(unsigned)gz;
-            *L(lds + FL_P2VS + v) = (int)(unsigned)gf;
+            *L(lds + fl_p2vs(PS) + v) = (int)(unsigned)gf;
           }
           ready = __ballot(!ok) == 0;
           if (!ready) __builtin_amdgcn_s_sleep(8);
@@ -1623,7 +1652,7 @@ __device__ __attribute__((noinline)) void fill_block_aff(kargs_c* ka, int blk, i
         q1 = q0;
       }
       // row 0 (stripe 0): Z = g col - oe (H = 0), F~ = -inf
-      p2_stage<2>(lds, s, nv, 16 * (q1 - q0), lane,
+      p2_stage<2, PS>(lds, s, nv, 16 * (q1 - q0), lane,
                   [&](int v, int k) { return k == 0 ? g * (cs + 16 * q0 + v) - oe : MSA_NEG; }, a.cod + a.cod_off,
                   a.cod_copy, cs, q0);
       const int flr0 = g * (64 * s + 1 + cs);
@@ -1633,7 +1662,7 @@ __device__ __attribute__((noinline)) void fill_block_aff(kargs_c* ka, int blk, i
         int INZ[16], INF[16];
         {
           const lds_int4* srz = reinterpret_cast<const lds_int4*>(L(lds + 16 * (q - q0)));
-          const lds_int4* srf = reinterpret_cast<const lds_int4*>(L(lds + FL_P2VS + 16 * (q - q0)));
+          const lds_int4* srf = reinterpret_cast<const lds_int4*>(L(lds + fl_p2vs(PS) + 16 * (q - q0)));
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const fl_v4i vz = srz[u], vf = srf[u];
@@ -1641,7 +1670,7 @@ __device__ __attribute__((noinline)) void fill_block_aff(kargs_c* ka, int blk, i
             INF[4 * u] = vf.x; INF[4 * u + 1] = vf.y; INF[4 * u + 2] = vf.z; INF[4 * u + 3] = vf.w;
           }
         }
-        const fl_v4u c4 = p2_codes(lds, q - q0, lane);
+        const fl_v4u c4 = p2_codes<PS>(lds, q - q0, lane);
         const unsigned cw[4] = {c4.x, c4.y, c4.z, c4.w};
         const int flq = flr0 + 16 * g * q;
         unsigned dw[4];
@@ -1687,7 +1716,7 @@ __device__ __attribute__((noinline)) void fill_block_aff(kargs_c* ka, int blk, i
     const int ob = __shfl_xor(bb, off), oi = __shfl_xor(bi, off), oj = __shfl_xor(bj, off);
     if (ob > bb || (ob == bb && (oi < bi || (oi == bi && oj < bj)))) { bb = ob; bi = oi; bj = oj; }
   }
-  if (lane == 0) a.blk[blk] = make_int4(bb, bi, bj, 0);
+  fl_block_result(a.blk, a.best_key, blk, lane, bb, bi, bj, a.n);
 }
 
 // Pass 2, affine, two rows per lane (R = 2: 128-row stripes, lane r holds rows 128s+2r+1 and
@@ -1697,6 +1726,7 @@ __device__ __attribute__((noinline)) void fill_block_aff(kargs_c* ka, int blk, i
 // one 2 KiB block (row-1 segments, then row-2 segments: traceback_kernel<TB_SW, 2>'s layout).
 template <int CALLER>
 __device__ __attribute__((noinline)) void fill_block_aff2(kargs_c* ka, int blk, int lane, lds_int* lds) {
+  constexpr int PS = fl_ps(CALLER);
   const FillArgs a = fill_args_of(ka);
   const unsigned ep = a.ep;
   const int m = a.m, n = a.n, S = (m + 127) / 128, g = a.g, oe = a.oe;
@@ -1704,9 +1734,9 @@ __device__ __attribute__((noinline)) void fill_block_aff2(kargs_c* ka, int blk, 
   int bb = INT32_MIN, bi = 0, bj = 0;
   if (s < S) {
     const int P = fl_P(s, m, n, 2);
-    const int q0 = seg * FL_PS;
+    const int q0 = seg * PS;
     if (q0 < P) {
-      int q1 = min(P, q0 + FL_PS);
+      int q1 = min(P, q0 + PS);
       const int cs = fl_cs(s);
       const int row_i = 128 * s + 2 * lane + 1;
       const unsigned ac = (row_i <= m) ? (a.A[a.a_off + row_i - 1] & 7u) : 0u;
@@ -1744,7 +1774,7 @@ __device__ __attribute__((noinline)) void fill_block_aff2(kargs_c* ka, int blk, 
             const unsigned long long gz = gload(brz + 16 * q0 + v), gf = gload(brf + 16 * q0 + v);
             ok = ok && ((unsigned)(gz >> 32) == ep) && ((unsigned)(gf >> 32) == ep);
             *L(lds + v) = (int)(unsigned)gz;
-            *L(lds + FL_P2VS + v) = (int)(unsigned)gf;
+            *L(lds + fl_p2vs(PS) + v) = (int)(unsigned)gf;
           }
           ready = __ballot(!ok) == 0;
           if (!ready) __builtin_amdgcn_s_sleep(8);
@@ -1755,7 +1785,7 @@ __device__ __attribute__((noinline)) void fill_block_aff2(kargs_c* ka, int blk, 
         q1 = q0;
       }
       // row 0 (stripe 0): Z = g col - oe (H = 0), F~ = -inf
-      p2_stage<2>(lds, s, nv, 16 * (q1 - q0), lane,
+      p2_stage<2, PS>(lds, s, nv, 16 * (q1 - q0), lane,
                   [&](int v, int k) { return k == 0 ? g * (cs + 16 * q0 + v) - oe : MSA_NEG; }, a.cod + a.cod_off,
                   a.cod_copy, cs, q0);
       const int flb = g * (128 * s + 1 + cs + lane);  // e(i+j) of row 1 at step 0 (row 2: + g)
@@ -1765,7 +1795,7 @@ __device__ __attribute__((noinline)) void fill_block_aff2(kargs_c* ka, int blk, 
         int INZ[16], INF[16];
         {
           const lds_int4* srz = reinterpret_cast<const lds_int4*>(L(lds + 16 * (q - q0)));
-          const lds_int4* srf = reinterpret_cast<const lds_int4*>(L(lds + FL_P2VS + 16 * (q - q0)));
+          const lds_int4* srf = reinterpret_cast<const lds_int4*>(L(lds + fl_p2vs(PS) + 16 * (q - q0)));
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const fl_v4i vz = srz[u], vf = srf[u];
@@ -1773,7 +1803,7 @@ __device__ __attribute__((noinline)) void fill_block_aff2(kargs_c* ka, int blk, 
             INF[4 * u] = vf.x; INF[4 * u + 1] = vf.y; INF[4 * u + 2] = vf.z; INF[4 * u + 3] = vf.w;
           }
         }
-        const fl_v4u c4 = p2_codes(lds, q - q0, lane);
+        const fl_v4u c4 = p2_codes<PS>(lds, q - q0, lane);
         const unsigned cw[4] = {c4.x, c4.y, c4.z, c4.w};
         const int flq = flb + 16 * g * q;
         unsigned dw1[4], dw2[4];
@@ -1839,11 +1869,11 @@ __device__ __attribute__((noinline)) void fill_block_aff2(kargs_c* ka, int blk, 
     const int ob = __shfl_xor(bb, off), oi = __shfl_xor(bi, off), oj = __shfl_xor(bj, off);
     if (ob > bb || (ob == bb && (oi < bi || (oi == bi && oj < bj)))) { bb = ob; bi = oi; bj = oj; }
   }
-  if (lane == 0) a.blk[blk] = make_int4(bb, bi, bj, 0);
+  fl_block_result(a.blk, a.best_key, blk, lane, bb, bi, bj, a.n);
 }
 
 // Pass 2, Gotoh (the reference's main_alignment_function path): block (stripe s, segment
-// seg) recomputes its FL_PS phases from SNAP (H~, R~, D~, diagonal H~ per lane) and the
+// seg) recomputes its PS phases from SNAP (H~, R~, D~, diagonal H~ per lane) and the
 // stripe above's bottom row (H~ and D~ granules) and writes the tag bytes (T1's, T2's, T3's
 // predecessor: the diagonal H~'s, the left R~'s and the upper D~'s tag) in the skewed stripe
 // layout.  The block holding cell (m, n) stores its three tables, unshifted, as the last
@@ -1851,15 +1881,16 @@ __device__ __attribute__((noinline)) void fill_block_aff2(kargs_c* ka, int blk, 
 // find_alignment's end rule from it).
 template <int CALLER>
 __device__ __attribute__((noinline)) void fill_block_got(kargs_c* ka, int blk, int lane, lds_int* lds) {
+  constexpr int PS = fl_ps(CALLER);
   const FillArgs a = fill_args_of(ka);
   const unsigned ep = a.ep;
   const int m = a.m, n = a.n, S = (m + 63) / 64, g = a.g, h4 = 4 * a.oe;
   const int s = blk / a.nseg, seg = blk - s * a.nseg;
   if (s < S) {
     const int P = fl_P(s, m, n, 1);
-    const int q0 = seg * FL_PS;
+    const int q0 = seg * PS;
     if (q0 < P) {
-      int q1 = min(P, q0 + FL_PS);
+      int q1 = min(P, q0 + PS);
       const int cs = fl_cs(s);
       const int row_i = 64 * s + lane + 1;
       const unsigned ac = (row_i <= m) ? (a.A[a.a_off + row_i - 1] & 7u) : 0u;
@@ -1899,7 +1930,7 @@ __device__ __attribute__((noinline)) void fill_block_got(kargs_c* ka, int blk, i
             const unsigned long long gz = gload(brz + 16 * q0 + v), gf = gload(brf + 16 * q0 + v);
             ok = ok && ((unsigned)(gz >> 32) == ep) && ((unsigned)(gf >> 32) == ep);
             *L(lds + v) = (int)(unsigned)gz;
-            *L(lds + FL_P2VS + v) = (int)(unsigned)gf;
+            *L(lds + fl_p2vs(PS) + v) = (int)(unsigned)gf;
           }
           ready = __ballot(!ok) == 0;
           if (!ready) __builtin_amdgcn_s_sleep(8);
@@ -1910,7 +1941,7 @@ __device__ __attribute__((noinline)) void fill_block_got(kargs_c* ka, int blk, i
         q1 = q0;
       }
       // row 0 (stripe 0), tagged and shifted: H~ 3 at column 0, 2 - 4h right of it; D~ 3 - 4h, 2 - 8h
-      p2_stage<2>(lds, s, nv, 16 * (q1 - q0), lane,
+      p2_stage<2, PS>(lds, s, nv, 16 * (q1 - q0), lane,
                   [&](int v, int k) {
                     const int col = cs + 16 * q0 + v;
                     return col < 0 ? MSA_NEG : (k == 0 ? (col == 0 ? 3 : 2 - h4) : (col == 0 ? 3 - h4 : 2 - 2 * h4));
@@ -1929,7 +1960,7 @@ __device__ __attribute__((noinline)) void fill_block_got(kargs_c* ka, int blk, i
         int INZ[16], INF[16];
         {
           const lds_int4* srz = reinterpret_cast<const lds_int4*>(L(lds + 16 * (q - q0)));
-          const lds_int4* srf = reinterpret_cast<const lds_int4*>(L(lds + FL_P2VS + 16 * (q - q0)));
+          const lds_int4* srf = reinterpret_cast<const lds_int4*>(L(lds + fl_p2vs(PS) + 16 * (q - q0)));
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const fl_v4i vz = srz[u], vf = srf[u];
@@ -1937,7 +1968,7 @@ __device__ __attribute__((noinline)) void fill_block_got(kargs_c* ka, int blk, i
             INF[4 * u] = vf.x; INF[4 * u + 1] = vf.y; INF[4 * u + 2] = vf.z; INF[4 * u + 3] = vf.w;
           }
         }
-        const fl_v4u c4 = p2_codes(lds, q - q0, lane);
+        const fl_v4u c4 = p2_codes<PS>(lds, q - q0, lane);
         const unsigned cw[4] = {c4.x, c4.y, c4.z, c4.w};
         unsigned dw[4];
 #pragma unroll
@@ -2014,15 +2045,16 @@ __device__ __attribute__((noinline)) void fill_block_got(kargs_c* ka, int blk, i
 // wave's row-1 16-byte segments, then its row-2 segments (traceback_kernel's R = 2 layout).
 template <int CALLER>
 __device__ __attribute__((noinline)) void fill_block_got2(kargs_c* ka, int blk, int lane, lds_int* lds) {
+  constexpr int PS = fl_ps(CALLER);
   const FillArgs a = fill_args_of(ka);
   const unsigned ep = a.ep;
   const int m = a.m, n = a.n, S = (m + 127) / 128, g = a.g, h4 = 4 * a.oe;
   const int s = blk / a.nseg, seg = blk - s * a.nseg;
   if (s < S) {
     const int P = fl_P(s, m, n, 2);
-    const int q0 = seg * FL_PS;
+    const int q0 = seg * PS;
     if (q0 < P) {
-      int q1 = min(P, q0 + FL_PS);
+      int q1 = min(P, q0 + PS);
       const int cs = fl_cs(s);
       const int row_i = 128 * s + 2 * lane + 1;
       const unsigned ac = (row_i <= m) ? (a.A[a.a_off + row_i - 1] & 7u) : 0u;
@@ -2062,7 +2094,7 @@ __device__ __attribute__((noinline)) void fill_block_got2(kargs_c* ka, int blk, 
             const unsigned long long gz = gload(brz + 16 * q0 + v), gf = gload(brf + 16 * q0 + v);
             ok = ok && ((unsigned)(gz >> 32) == ep) && ((unsigned)(gf >> 32) == ep);
             *L(lds + v) = (int)(unsigned)gz;
-            *L(lds + FL_P2VS + v) = (int)(unsigned)gf + h4;
+            *L(lds + fl_p2vs(PS) + v) = (int)(unsigned)gf + h4;
           }
           ready = __ballot(!ok) == 0;
           if (!ready) __builtin_amdgcn_s_sleep(8);
@@ -2073,7 +2105,7 @@ __device__ __attribute__((noinline)) void fill_block_got2(kargs_c* ka, int blk, 
         q1 = q0;
       }
       // row 0 (stripe 0), tagged and shifted: H~ 3 at column 0, 2 - 4h right of it; D~ + 4h 3, 2 - 4h
-      p2_stage<2>(lds, s, nv, 16 * (q1 - q0), lane,
+      p2_stage<2, PS>(lds, s, nv, 16 * (q1 - q0), lane,
                   [&](int v, int k) {
                     const int col = cs + 16 * q0 + v;
                     return col < 0 ? MSA_NEG : (k == 0 ? (col == 0 ? 3 : 2 - h4) : (col == 0 ? 3 : 2 - h4));
@@ -2091,7 +2123,7 @@ __device__ __attribute__((noinline)) void fill_block_got2(kargs_c* ka, int blk, 
         int INZ[16], INF[16];
         {
           const lds_int4* srz = reinterpret_cast<const lds_int4*>(L(lds + 16 * (q - q0)));
-          const lds_int4* srf = reinterpret_cast<const lds_int4*>(L(lds + FL_P2VS + 16 * (q - q0)));
+          const lds_int4* srf = reinterpret_cast<const lds_int4*>(L(lds + fl_p2vs(PS) + 16 * (q - q0)));
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const fl_v4i vz = srz[u], vf = srf[u];
@@ -2099,7 +2131,7 @@ __device__ __attribute__((noinline)) void fill_block_got2(kargs_c* ka, int blk, 
             INF[4 * u] = vf.x; INF[4 * u + 1] = vf.y; INF[4 * u + 2] = vf.z; INF[4 * u + 3] = vf.w;
           }
         }
-        const fl_v4u c4 = p2_codes(lds, q - q0, lane);
+        const fl_v4u c4 = p2_codes<PS>(lds, q - q0, lane);
         const unsigned cw[4] = {c4.x, c4.y, c4.z, c4.w};
         unsigned dw1[4], dw2[4];
         // four cells' direction bytes, tags of their inputs H~ diag | R~ left << 2 | D~ up << 4: the
@@ -2212,7 +2244,7 @@ __global__ __launch_bounds__(FL_FILLW * 64) __attribute__((amdgpu_waves_per_eu(F
   const int lane = threadIdx.x & 63;
   const int w = uni(threadIdx.x >> 6);
   kargs_c* ka = (kargs_c*)__builtin_amdgcn_kernarg_segment_ptr();  // (a is the only argument)
-  lds_int* wl = L(smem + w * FL_P2INTS);
+  lds_int* wl = L(smem + w * fl_p2ints(FL_PS_FILL));
   for (;;) {
     int t = 0;
     if (lane == 0) t = atomicAdd(a.ticket + MSA_TK_BLOCK, 1);

@@ -73,6 +73,8 @@
 #define MSA_NTICKET 128      // run tickets (ints): [0] stripe_kernel, [4..11] flow item chunks,
 #define MSA_TK_ARRIVE 32     // flow kernel: arrival order (pass-1 / pass-2 role), own 128-B line
 #define MSA_TK_BLOCK 64      // flow kernel: pass-2 blocks, own 128-B line
+#define MSA_TK_BEST 96       // flow kernel, fused reduction: the best block key (u64), own 128-B line
+#define MSA_TK_DONE 100      //   and the finished pass-2 blocks
 #define MSA_CPAD 256         // code segment padding (bytes) on each side of a pair's columns
 #define MSA_NCOPY 16         // byte-shifted code copies: every lane reads 16-byte aligned dwordx4
 #define MSA_CRING 1024       // single-pair LDS code ring: columns per copy (+64 B mirror), 4 copies
@@ -172,10 +174,11 @@ struct KArgs {
   // two-pass single pair (msa_flow.hip)
   // {epoch, value} granules: pass-2 blocks run while pass 1 is still producing
   unsigned long long* br;    // [S][brw] bottom row of every stripe
-  unsigned long long* snap;  // [S][nseg][2][64] lane states at every FL_PS-th phase
+  unsigned long long* snap;  // [S][nseg][2][64] lane states at the start of every pass-2 segment
   int4* blk;                 // [S * nseg] pass-2 block bests
   const int* border;         // pass-2 blocks in expected readiness order
   int brw, nseg, nblk;
+  int ps_shift;              // log2 of the phases per pass-2 segment (pass 1 saves SNAP that often)
   int nflow;                 // workgroups [0, nflow) run pass 1, the rest pass-2 blocks
   // chunked banded mode (kp.single == 2)
   int* ck;                   // [chunk][2: warm-up end, chunk end][2: H, F][ckw] band states
@@ -184,6 +187,9 @@ struct KArgs {
   // chunked banded mode with int16 chunk cells: chunks >= 1 write H relative to their guessed row as
   // int16 here ([stripe - chunk_c][pmax * 16 * 64], the outH cell order); chunk_add_kernel widens them
   int16_t* outH16;
+  // two-pass SW single pair: the pass-2 blocks fold the pair result into this key themselves
+  // (fl_block_result, msa_flow.hip) when set; else reduce_blocks_kernel runs after the launch
+  unsigned long long* best_key;
 };
 #ifndef MSA_H16_PAIRED
 #define MSA_H16_PAIRED 1  // int16 chunk cells: two u-blocks of a lane per 16 B (msa_band.hip)
@@ -1487,6 +1493,24 @@ struct PairResult {
   int32_t fin[3];
   int32_t pad;
 };
+
+// A two-pass SW plan's best-cell key (fl_block_result, msa_flow.hip): score ^ 2^31 in the high word,
+// ~(i (n + 1) + j) of the first best cell in row-major order in the low word; a score <= 0 keeps the
+// end at (0, 0), reduce_blocks_kernel's rule.
+__host__ __device__ inline PairResult best_key_decode(unsigned long long k, long long n) {
+  PairResult r;
+  r.score = (int32_t)((uint32_t)(k >> 32) ^ 0x80000000u);
+  r.status = 0;
+  const unsigned long long lin = (unsigned long long)(~(uint32_t)k);
+  r.end_i = r.score > 0 ? (int64_t)(lin / (unsigned long long)(n + 1)) : 0;
+  r.end_j = r.score > 0 ? (int64_t)(lin % (unsigned long long)(n + 1)) : 0;
+  r.fin[0] = r.fin[1] = r.fin[2] = 0;
+  r.pad = 0;
+  return r;
+}
+__global__ void best_key_kernel(const unsigned long long* key, long long n, PairResult* out) {
+  if (threadIdx.x == 0) out[0] = best_key_decode(*key, n);
+}
 
 // ---------------------------------------------------------------------------
 // Chunked banded mode (kp.single == 2), after the chunk launch.

@@ -172,11 +172,13 @@ __global__ __launch_bounds__(64) void traceback_kernel(const uint8_t* __restrict
                                                        const msa_stripe_meta* __restrict__ meta,
                                                        const PairResult* __restrict__ res, int pair, int end_type,
                                                        int hpen, uint8_t* __restrict__ ops, long long cap,
-                                                       long long* __restrict__ info, int csflow) {
+                                                       long long* __restrict__ info, int csflow,
+                                                       const unsigned long long* __restrict__ best_key) {
   constexpr bool REF = KIND != TB_SW;
   const int lane = threadIdx.x;
   const msa_pair_desc pd = pairs[pair];
-  const PairResult r0 = res[pair];
+  // (a two-pass SW plan whose pass-2 blocks folded the result into the best-cell key: no PairResult)
+  const PairResult r0 = (!REF && best_key) ? best_key_decode(*best_key, pd.n) : res[pair];
   const uint8_t* base = dir + pd.out_off + lane * 16;
   const int pmax = pd.pmax;
   // plans hold m, n < 2^26

@@ -71,6 +71,12 @@ int msa_device_count(int* count);
  * last set, calls that had to wait, calls admitted}. */
 int msa_set_device_budget(int64_t bytes);
 int msa_device_budget_info(int64_t* out5);
+/* Memory held on the current device: out4 = {bytes admitted now, idle cached plans of the
+ * reference walk (footprint estimate), free blocks of the device pool, admissions that released
+ * the idle ones first}.  An admission that would put admitted + idle bytes over the budget first
+ * destroys the idle cached plans and frees the pool's blocks.  Plans created directly through
+ * msa_plan_create (the device-resident API below) are the caller's and are not admitted. */
+int msa_device_memory_info(int64_t* out4);
 
 /* Node of an alignment path: the reference's `align` struct
  * (subproblem_alignment.h:8-13) without the `next` pointer. */
