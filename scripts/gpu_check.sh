@@ -14,6 +14,8 @@ if [ -n "$TESTS" ] || [ -n "$K" ]; then
   rc=$?
   tail -3 gpurun_out/${TAG}_tests.log
   [ $rc -eq 0 ] || [ $rc -eq 1 ] || stop tests $rc
+  # a per-test time limit (pytest-timeout, thread method) also exits 1: a hung GPU test ends the script
+  grep -q "+++ Timeout +++" gpurun_out/${TAG}_tests.log && stop "tests (a test hit its time limit)" $rc
   [ $rc -eq 1 ] && grep -E "^(FAILED|ERROR)|Error" gpurun_out/${TAG}_tests.log | head -20
 fi
 IFS=';' read -ra BL <<< "$BENCHES"
