@@ -512,7 +512,7 @@ def main():
         tb_ms = e0.elapsed_time(e1) / 5
         inf = tb_info.cpu().tolist()
         tb_walk = dict(ops=inf[0], group_switches=inf[4], fetched_on_demand=inf[5], memtime_ticks=inf[6],
-                       wait_ticks=inf[7])
+                       loader_requests=inf[7])
     if plan.error():
         raise SystemExit(f"rank {rank}: a kernel wait hit its spin limit in the timing pass")
 

@@ -199,7 +199,7 @@ class Plan:
         LB.check(int(inf[3]), "msa_plan_traceback")
         o = bytes(ops[:inf[0]].cpu().numpy().tobytes())
         return dict(ops=o, beg=(int(inf[1]), int(inf[2])), cigar=cigar_of(o),
-                    stats=dict(switches=int(inf[4]), on_demand=int(inf[5]), ticks=int(inf[6]), wait_ticks=int(inf[7])))
+                    stats=dict(switches=int(inf[4]), on_demand=int(inf[5]), ticks=int(inf[6]), requests=int(inf[7])))
 
     def traceback_gotoh_async(self, dDir, d_ops, d_info, end_type=-1, pair=0, stream=None) -> None:
         """Device find_alignment walk (msa_plan_traceback_gotoh) of a REF_GOTOH DIR plan, stream-ordered after

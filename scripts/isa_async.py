@@ -175,10 +175,13 @@ def scan(so: Path, prefixes=None, workers=1):
              if not prefixes or name.startswith(prefixes)]
     if workers <= 1:
         return dict(map(_analyse_item, items))
+    import multiprocessing
     from concurrent.futures import ProcessPoolExecutor
 
     items.sort(key=lambda it: -len(it[1]))  # largest first: the long kernels set the wall time
-    with ProcessPoolExecutor(workers) as ex:
+    # spawned workers: a forked child would inherit the HIP runtime a loaded libmsa.so started in this
+    # process, and the parent then faulted at interpreter exit (the CPU suite's exit status 139)
+    with ProcessPoolExecutor(workers, mp_context=multiprocessing.get_context("spawn")) as ex:
         return dict(ex.map(_analyse_item, items, chunksize=1))
 
 

@@ -15,7 +15,8 @@ LLVM = Path("/opt/rocm/lib/llvm/bin")
 def kernels(so: Path):
     with tempfile.TemporaryDirectory() as td:
         fat, co = Path(td) / "fat.bin", Path(td) / "co.o"
-        subprocess.run(["objcopy", f"--dump-section=.hip_fatbin={fat}", str(so)], check=True)
+        subprocess.run(["objcopy", f"--dump-section=.hip_fatbin={fat}", str(so), str(fat) + ".elf"],
+                       check=True)  # (an output file: without one objcopy rewrites the library in place)
         subprocess.run([str(LLVM / "clang-offload-bundler"), "--type=o", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950",
                         f"--input={fat}", f"--output={co}", "--unbundle"], check=True)
         txt = subprocess.run([str(LLVM / "llvm-readelf"), "--notes", str(co)], check=True, capture_output=True,

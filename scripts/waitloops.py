@@ -21,7 +21,8 @@ BR = re.compile(r"<([^>+]+)\+0x([0-9a-f]+)>|<([^>]+)>")
 def disassemble(so: Path) -> str:
     with tempfile.TemporaryDirectory() as td:
         fat, co = Path(td) / "fat.bin", Path(td) / "co.o"
-        subprocess.run(["objcopy", f"--dump-section=.hip_fatbin={fat}", str(so)], check=True)
+        subprocess.run(["objcopy", f"--dump-section=.hip_fatbin={fat}", str(so), str(fat) + ".elf"],
+                       check=True)  # (an output file: without one objcopy rewrites the library in place)
         subprocess.run([str(LLVM / "clang-offload-bundler"), "--type=o", f"--targets={TARGET}", f"--input={fat}",
                         f"--output={co}", "--unbundle"], check=True)
         return subprocess.run([str(LLVM / "llvm-objdump"), "-d", "--mcpu=gfx950", str(co)], check=True,

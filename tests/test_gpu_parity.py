@@ -1098,6 +1098,37 @@ def test_walks_across_long_gaps(oracle, dev, LB, gap):
                                                                            o2["cigar"])
 
 
+@pytest.mark.parametrize("off", [0, 1, 7])
+def test_walk_ops_unaligned_and_capped(oracle, dev, LB, off):
+    """The walk's decoder wave writes diagonal runs (up to 128 'M') with 16-byte stores between byte-wise head
+    and tail: into an ops buffer at any byte offset, and with a capacity below the op count, the bytes written
+    are the oracle's ops up to the capacity (status MSA_ERR_CAPACITY when short) and no byte outside the
+    buffer changes."""
+    import torch
+    from cse305_parallel_sequence_alignment_amd.plan import Plan
+
+    rng = np.random.default_rng(91 + off)
+    A, B = _mutated(rng, 3000, 3050)
+    m, n = len(A), len(B)
+    pl = Plan(LB.REF_GOTOH, LB.CELLS_DIR, [m], [n], [0], [0], match=1, mismatch=0, gap_open=3, gap_extend=1,
+              start_type=-1)
+    D = torch.empty(pl.cells_elems, dtype=torch.uint8, device=dev)
+    pl.run(_dev(A, dev), _dev(B, dev), D)
+    o = oracle.subproblem_align(A, B, -1, -1, 1.0, 2.0)
+    want = "".join("MDI"[t - 1] for (_, _, t) in reversed(o["nodes"])).encode()
+    for cap in (len(want) + 5, len(want), len(want) - 37, 21):
+        big = torch.full((off + cap + 64,), 0xAA, dtype=torch.uint8, device=dev)
+        info = torch.zeros(8, dtype=torch.int64, device=dev)
+        pl.traceback_gotoh_async(D, big[off:off + cap], info, -1)
+        inf = info.cpu().tolist()
+        got = big.cpu().numpy().tobytes()
+        assert inf[0] == len(want), (off, cap)
+        assert inf[3] == (0 if cap >= len(want) else -8), (off, cap, inf[3])
+        k = min(cap, len(want))
+        assert got[off:off + k] == want[:k], (off, cap)
+        assert got[:off] == b"\xaa" * off and got[off + k:] == b"\xaa" * (len(got) - off - k), (off, cap)
+
+
 def test_gotoh_walk_rejects_wrong_plans(dev, LB):
     """msa_plan_traceback_gotoh needs a REF_GOTOH DIR plan and a valid end type; msa_plan_traceback needs an
     SW-affine DIR plan created with track_end (its walk starts at the fill's end cell)."""
