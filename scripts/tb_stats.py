@@ -21,6 +21,7 @@ from cse305_parallel_sequence_alignment_amd.plan import Plan
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--workload", default="c5", choices=["c5", "ref", "refwhole"])
+ap.add_argument("--trace", default="", help="save the event traces (.npz)")
 args = ap.parse_args()
 if args.workload == "c5":
     A, B = data.c5_pair(0)
@@ -36,7 +37,7 @@ dA = torch.from_numpy(data.encode(A)).cuda()
 dB = torch.from_numpy(data.encode(B)).cuda()
 out = torch.empty(pl.cells_elems, dtype=torch.uint8, device="cuda")
 ops = torch.empty(len(A) + len(B) + 16, dtype=torch.uint8, device="cuda")
-info = torch.zeros(18, dtype=torch.int64, device="cuda")
+info = torch.zeros(32 + 2 * 16384, dtype=torch.int64, device="cuda")
 pl.run(dA, dB, out)
 rows, ms = [], []
 for rep in range(4):
@@ -48,11 +49,18 @@ for rep in range(4):
         pl.traceback_gotoh_async(out, ops, info, -1)
     e1.record()
     torch.cuda.synchronize()
-    rows.append(info.cpu().tolist())
+    rows.append(info.cpu().tolist() if rep == 3 else info[:32].cpu().tolist())
     ms.append(e0.elapsed_time(e1))
 k = rows[-1]
+if args.trace:
+    # event traces of the last walk: walker group lookups {t << 32 | s, asked, ready word seen, got},
+    # loader groups {b0 << 32 | s, issue start, issue end, published}
+    import numpy as np
+    tr = np.array(k[32:32 + 16384], dtype=np.int64).reshape(-1, 4)
+    lg = np.array(k[32 + 16384:], dtype=np.int64).reshape(-1, 4)
+    np.savez(args.trace, walker=tr[:min(k[12] + k[13] + 64, 4096)], loader=lg[:min(k[17], 4096)])
 assert k[3] == 0, f"walk status {k[3]}"
 print(json.dumps(dict(workload=args.workload, ops=k[0], t_total=k[8], t_wait=k[4], t_in_groups=k[7],
                       t_runs=k[10], t_decoder=k[11], n_run=k[5], n_win=k[6], n_switch=k[12], n_demand=k[9],
-                      n_req=k[13], ld_issue=k[14], ld_wait=k[15], ld_issue_to_publish=k[16], ld_groups=k[17],
+                      n_req=k[13], ld_issue=k[14], ld_wait=k[15], ld_issue_to_publish=k[16], ld_groups=k[17], ld_paths=k[18:22], ld_path_ticks=k[22:26], ld_sel_ticks=k[26], ld_sels=k[27],
                       walk_ms=[round(x, 4) for x in ms])), flush=True)
