@@ -1492,7 +1492,7 @@ int msa_plan_traceback(msa_plan* P, int64_t pair, const uint8_t* dDir, uint8_t* 
   if (P->kp.alg != MSA_ALG_SWA || P->d.cells != MSA_CELLS_DIR || !P->d.track_end) return MSA_ERR_UNSUPPORTED;
   hipStream_t st = (hipStream_t)stream;
   P->note_stream(st);
-  hipLaunchKernelGGL((P->R == 2 ? traceback_kernel<TB_SW, 2> : traceback_kernel<TB_SW>), dim3(1), dim3(192), 0, st, dDir, P->d_pairs, P->d_meta,
+  hipLaunchKernelGGL((P->R == 2 ? traceback_kernel<TB_SW, 2> : traceback_kernel<TB_SW>), dim3(1), dim3(384), 0, st, dDir, P->d_pairs, P->d_meta,
                      (const PairResult*)P->d_res, (int)pair, 0, 0, d_ops, (long long)ops_cap, (long long*)d_info,
                      P->flow ? 1 : 0,
                      P->fused_reduce ? reinterpret_cast<const unsigned long long*>(P->d_ticket + MSA_TK_BEST) : nullptr);
@@ -1511,7 +1511,7 @@ int msa_plan_traceback_gotoh(msa_plan* P, int64_t pair, int end_type, const uint
   // REF1 bytes hold tags (3 / 2 / 1 = T1 / T2 / T3), REF bytes the table numbers
   hipLaunchKernelGGL(P->kp.alg == MSA_ALG_REF1 ? (P->R == 2 ? traceback_kernel<TB_REF_TAG, 2> : traceback_kernel<TB_REF_TAG>)
                                                : traceback_kernel<TB_REF>, dim3(1),
-                     dim3(192), 0, st, dDir, P->d_pairs, P->d_meta, (const PairResult*)P->d_res, (int)pair, end_type,
+                     dim3(384), 0, st, dDir, P->d_pairs, P->d_meta, (const PairResult*)P->d_res, (int)pair, end_type,
                      (int)P->kp.h, d_ops, (long long)ops_cap, (long long*)d_info, P->flow ? 1 : 0,
                      (const unsigned long long*)nullptr);
   HIPCHK(hipGetLastError());

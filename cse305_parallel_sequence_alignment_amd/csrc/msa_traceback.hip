@@ -169,11 +169,11 @@ __device__ __forceinline__ bool tb_diag_stay(unsigned dv) {
 // Hand-off words between the walk's three waves (LDS; see traceback_kernel).
 struct TbCtl {
   unsigned long long ready[4];  // per slot: the group that has landed there, (b0 << 32) | stripe
-  int req_seq, req_s, req_t;    // walker -> loader: stage stripe s's group covering step t
+  int req_seq[4], req_s[4], req_t[4];  // walker -> loader s & 3: stage stripe s's group covering step t
   int ent_seq, ent_s, ent_col;  // walker -> loader: entered stripe s at column j - r (the prefetch hint)
   int consumed;                 // decoder -> walker: ring words decoded (their entries are free again)
   int done, nw_total;           // walker: finished, after nw_total words
-  int n_demand;                 // loader: groups staged because a request found none covering
+  int n_demand[4];              // loaders: groups staged because a request found none covering
   long long nops, t_dec;        // decoder: ops decoded; busy ticks (diagnostic build)
   int wi, wj, wstatus, n_switch, n_req;  // walker: where it stopped, status, stripes entered, requests
   long long t_walk, wst[5];              // walker: ticks; diagnostic build: wait, runs, windows, in groups, in runs
@@ -209,17 +209,18 @@ constexpr int TB_SPIN_MAX = 1 << 24;
 // two-rows-per-lane Gotoh flow fill (128-row stripes, lane r holds rows 2r+1 and 2r+2 at column
 // cs + t - r; a 16-step block is 2 KiB: the row-1 segments, then the row-2 segments).
 //
-// One workgroup of three waves.  Wave 1 walks; its state is uniform (SGPRs) and it touches LDS
-// only.  Wave 0 stages stripe groups into LDS: on the walker's request (stripe s, step t: the
+// One workgroup of six waves.  Wave 1 walks; its state is uniform (SGPRs) and it touches LDS
+// only.  Waves 0, 3, 4, 5 stage stripe groups into LDS, one slot (stripe mod 4) each (each its own
+// vmcnt and issue stalls: a loader stages one group per four stripes): on the walker's request (stripe s, step t: the
 // group covering t) and, each time the walker enters a stripe, the next three stripes' predicted
-// groups; it publishes a group in ready[slot] once its loads have landed (its own s_waitcnt), so
-// the issue stalls of 16-32 KiB of LDS-DMA per stripe and the load latency stay off the walk.
-// (The loader is wave 0: an LDS-DMA lane writes M0 + 16 x its thread id.)  Wave 2 decodes the
-// walker's LDS ring of step words into op bytes while the walk goes on.  Every wave's loop ends: the walker's waits are
-// bounded (TB_SPIN_MAX), and waves 0 and 2 leave after the walker's `done`, wave 0 with none of
-// its loads in flight.
+// groups; a loader publishes a group in ready[slot] once its loads have landed (its own
+// s_waitcnt), so the issue stalls of 16-32 KiB of LDS-DMA per stripe and the load latency stay off
+// the walk (an LDS-DMA lane writes M0 + 16 x its lane: mbench/mb_dma.hip).  Wave 2 decodes the
+// walker's LDS ring of step words into op bytes while the walk goes on.  Every wave's loop ends:
+// the walker's waits are bounded (TB_SPIN_MAX), and the other waves leave after the walker's
+// `done`, the loaders with none of their loads in flight.
 template <int KIND, int RL = 1>
-__global__ __launch_bounds__(192) void traceback_kernel(const uint8_t* __restrict__ dir,
+__global__ __launch_bounds__(384) void traceback_kernel(const uint8_t* __restrict__ dir,
                                                         const msa_pair_desc* __restrict__ pairs,
                                                         const msa_stripe_meta* __restrict__ meta,
                                                         const PairResult* __restrict__ res, int pair, int end_type,
@@ -253,11 +254,12 @@ __global__ __launch_bounds__(192) void traceback_kernel(const uint8_t* __restric
   __shared__ unsigned rawl[TB_RAW];
   __shared__ TbCtl ctl_s;
   if (!csflow)
-    for (int k = threadIdx.x; k < S && k < TB_CSL; k += 192) csl[k] = meta[pd.stripe0 + k].cs;
-  for (int k = threadIdx.x; k < TB_RAW; k += 192) rawl[k] = 0u;
+    for (int k = threadIdx.x; k < S && k < TB_CSL; k += 384) csl[k] = meta[pd.stripe0 + k].cs;
+  for (int k = threadIdx.x; k < TB_RAW; k += 384) rawl[k] = 0u;
   if (threadIdx.x == 0) {
     for (int k = 0; k < NSLOT; ++k) ctl_s.ready[k] = ~0ull;  // stripe -1: empty
-    ctl_s.req_seq = ctl_s.ent_seq = ctl_s.consumed = ctl_s.done = ctl_s.nw_total = ctl_s.n_demand = 0;
+    for (int k = 0; k < 4; ++k) ctl_s.req_seq[k] = ctl_s.n_demand[k] = 0;
+    ctl_s.ent_seq = ctl_s.consumed = ctl_s.done = ctl_s.nw_total = 0;
     ctl_s.nops = ctl_s.t_dec = 0;
   }
   __syncthreads();
@@ -283,8 +285,11 @@ __global__ __launch_bounds__(192) void traceback_kernel(const uint8_t* __restric
     d = k == 3 ? v : d;
   };
 
-  if (wave == 0) {
-    // ---- loader: stage groups, publish them once landed ----
+  if (wave != 1 && wave != 2) {
+    // ---- loaders: stage groups, publish them once landed; wave 0 the stripes s = 0 mod 4 (slot 0),
+    // waves 3, 4, 5 those of slots 1, 2, 3 (each its own vmcnt and issue stalls: a loader stages one
+    // group per four stripes) ----
+    const int par = __builtin_amdgcn_readfirstlane(wave == 0 ? 0 : wave - 2);  // (uniform: M0 and the SGPR operands)
     // slot bookkeeping (slot = stripe & 3): the stripe staged there, its first block, the count
     // of loads issued up to its own (its loads are complete once at most `issued - end` later
     // loads are outstanding), and whether it has been published
@@ -354,11 +359,11 @@ __global__ __launch_bounds__(192) void traceback_kernel(const uint8_t* __restric
         }
     };
     for (;;) {
-      const int rq = tb_u(ctl_s.req_seq);
+      const int rq = tb_u(ctl_s.req_seq[par]);
       if (rq != last_req) {
         // the walker waits for stripe s's group covering step t
         last_req = rq;
-        const int s = tb_u(ctl_s.req_s), t = tb_u(ctl_s.req_t);
+        const int s = tb_u(ctl_s.req_s[par]), t = tb_u(ctl_s.req_t[par]);
         const int k = s & (NSLOT - 1);
         const int b0 = sel4(k, sl_b0, sl_b1, sl_b2, sl_b3);
         if (sel4(k, sl_s0, sl_s1, sl_s2, sl_s3) != s || t < 16 * b0 || t >= 16 * b0 + GT) {
@@ -381,6 +386,7 @@ __global__ __launch_bounds__(192) void traceback_kernel(const uint8_t* __restric
         for (int d = 1; d <= NSLOT - 1; ++d) {
           const int sd = s - d;
           if (sd < 0) break;
+          if ((sd & 3) != par) continue;  // (another loader's stripe)
           if (sel4(sd & (NSLOT - 1), sl_s0, sl_s1, sl_s2, sl_s3) == sd) continue;
           stage_group(sd, group_b0(RL == 2 ? col - 128 * d + 190 - cs_of(sd) : col - 64 * d + 126 - cs_of(sd)));
         }
@@ -400,7 +406,7 @@ __global__ __launch_bounds__(192) void traceback_kernel(const uint8_t* __restric
       __builtin_amdgcn_s_sleep(1);
     }
     vm_wait_all();  // no load left in flight when the wave ends
-    tb_st(ctl_s.n_demand, n_demand);
+    tb_st(ctl_s.n_demand[par], n_demand);
 #ifdef MSA_TB_STATS
     tb_st(ctl_s.lst[0], t_iss);
     tb_st(ctl_s.lst[1], t_lw);
@@ -504,9 +510,9 @@ __global__ __launch_bounds__(192) void traceback_kernel(const uint8_t* __restric
         const long long a = (long long)__builtin_amdgcn_s_memtime();
 #endif
         ++n_req;
-        tb_st(ctl_s.req_s, s);
-        tb_st(ctl_s.req_t, t);
-        tb_st(ctl_s.req_seq, ++rseq);
+        tb_st(ctl_s.req_s[s & 3], s);
+        tb_st(ctl_s.req_t[s & 3], t);
+        tb_st(ctl_s.req_seq[s & 3], ++rseq);  // (one counter: a channel's values still change on every request)
         for (int spin = 0; !covers(v, s, t); ++spin) {
           if (spin > TB_SPIN_MAX) { status = MSA_ERR_TIMEOUT; break; }
           v = tb_u64(ctl_s.ready[s & (NSLOT - 1)]);
@@ -706,7 +712,7 @@ __global__ __launch_bounds__(192) void traceback_kernel(const uint8_t* __restric
     info[6] = ctl_s.wst[2];
     info[7] = ctl_s.wst[3];
     info[8] = ctl_s.t_walk;
-    info[9] = ctl_s.n_demand;
+    info[9] = ctl_s.n_demand[0] + ctl_s.n_demand[1] + ctl_s.n_demand[2] + ctl_s.n_demand[3];
     info[10] = ctl_s.wst[4];
     info[11] = ctl_s.t_dec;
     info[12] = ctl_s.n_switch;
@@ -717,7 +723,7 @@ __global__ __launch_bounds__(192) void traceback_kernel(const uint8_t* __restric
     info[17] = ctl_s.lst[3];
 #else
     info[4] = ctl_s.n_switch;
-    info[5] = ctl_s.n_demand;  // groups staged on request (the first, mispredictions, walks leaving a group)
+    info[5] = ctl_s.n_demand[0] + ctl_s.n_demand[1] + ctl_s.n_demand[2] + ctl_s.n_demand[3];  // groups staged on request (the first, mispredictions, walks leaving a group)
     info[6] = ctl_s.t_walk;    // s_memtime ticks, the walk's start to its last step
     info[7] = ctl_s.n_req;     // times the walker waited for the loader
 #endif
