@@ -286,13 +286,14 @@ int64_t msa_plan_stripes(const msa_plan* plan);
 int msa_plan_pair_layout(const msa_plan* plan, int64_t pair, int64_t* out4);
 /* Smith-Waterman traceback ON THE DEVICE (msa_traceback.hip), for an
  * MSA_SW_AFFINE plan with MSA_CELLS_DIR after msa_plan_run on the same stream:
- * one wave walks pair `pair`'s direction bytes dDir from the end cell the run
+ * one workgroup (a walker wave, four stripe-group loader waves, an op decoder
+ * wave) walks pair `pair`'s direction bytes dDir from the end cell the run
  * found (first maximum, row-major) and writes the ops end -> start into d_ops
  * ('M' diagonal, 'D' gap consuming B, 'I' gap consuming A; at most ops_cap,
- * m+n suffices) and d_info[8] = {n_ops, beg_i, beg_j, status, group
- * switches, of them fetched on demand, s_memtime ticks of the walk, of them
- * waiting for loads} (beg = the first aligned cell, 1-based; status 0 or
- * MSA_ERR_CAPACITY).  Asynchronous,
+ * m+n suffices) and d_info[8] = {n_ops, beg_i, beg_j, status, stripes
+ * entered, groups staged on demand, s_memtime ticks of the walk, times the
+ * walker waited for a loader} (beg = the first aligned cell, 1-based; status
+ * 0, MSA_ERR_CAPACITY or MSA_ERR_TIMEOUT).  Asynchronous,
  * no host sync; tie order of the oracle's orc_sw. */
 int msa_plan_traceback(msa_plan* plan, int64_t pair, const uint8_t* dDir, uint8_t* d_ops, int64_t ops_cap,
                        int64_t* d_info, void* stream);
