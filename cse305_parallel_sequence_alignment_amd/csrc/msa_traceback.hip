@@ -430,14 +430,6 @@ __global__ __launch_bounds__(384) void traceback_kernel(const uint8_t* __restric
         __builtin_amdgcn_s_sleep(2);
         continue;
       }
-#ifdef MSA_TB_DECBATCH
-      if (nq < 32 && !dn) {
-        // fewer than half a wave of words: let them gather (a word per lane; the walker writes one every
-        // few hundred ticks, and a batch of one or two kept this wave ~90% busy)
-        __builtin_amdgcn_s_sleep(8);
-        continue;
-      }
-#endif
 #ifdef MSA_TB_STATS
       const long long td0 = (long long)__builtin_amdgcn_s_memtime();
 #endif
