@@ -1,4 +1,5 @@
 # device walk: walk parity tests, walk stats (diagnostic build vlib/libmsa_tbstats.so), c5 / ref / 97k benches
+# (build the diagnostic library first, on the CPU: scripts/build_variant.sh tbstats -DMSA_TB_STATS)
 set -o pipefail
 mkdir -p gpurun_out
 K="traceback or walk or gotoh or ref or c5 or affine or capped" TESTS= bash scripts/gpu_check.sh walk || exit 2
